@@ -1,0 +1,195 @@
+/*
+ * vdiff.h -- C-ABI of libvdiff.so, the MI355X (gfx950) kernels behind the
+ * video-diffusion denoiser hot path of wdas03/lipreading-video-generation.
+ *
+ * The reference has no FFI: its boundary is the Python module API of
+ * video-generation/diffusion (unet.py, unet_audio.py, utils.py,
+ * linear_noise_scheduler.py, noise_scheduler.py).  Every entry point below
+ * replaces the ATen op(s) that the reference calls at the cited line; the
+ * Python drop-in (lipreading-video-generation_amd/video-generation/diffusion)
+ * binds them through ctypes.
+ *
+ * Conventions
+ *  - All tensor arguments are caller-owned DEVICE pointers.  The library never
+ *    allocates device memory; kernels that need scratch take a workspace
+ *    pointer whose size is returned by the matching *_workspace_size().
+ *  - Activations are channels-last: a [B, C, T, H, W] tensor is stored as
+ *    [B][T][H][W][C] (C fastest).  2-D tensors use T = 1.
+ *  - `stream` is a hipStream_t passed as void* (0 = null stream).  Every call
+ *    is asynchronous and stream-ordered; nothing synchronises the host.
+ *  - Return 0 on success, otherwise a VD_E* code; vd_last_error() returns a
+ *    thread-local message describing the last failure.
+ *  - dtype: VD_F32 (parity mode, fp32 storage, exact-fp32 MFMA / VALU math) or
+ *    VD_BF16 (throughput mode, bf16 storage, fp32 accumulate/statistics).
+ */
+#ifndef VDIFF_H
+#define VDIFF_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VDIFF_ABI_VERSION 1
+
+enum vd_status { VD_OK = 0, VD_EINVAL = 1, VD_EUNSUPPORTED = 2, VD_ELAUNCH = 3 };
+enum vd_dtype { VD_F32 = 0, VD_BF16 = 1 };
+
+/* ---- library ---------------------------------------------------------- */
+int vd_version(void);
+const char* vd_last_error(void);
+/* Writes "name;gfx;CUs;HBM bytes" of the current device into buf. */
+int vd_device_info(char* buf, int buflen);
+
+/* ---- timestep embedding ------------------------------------------------
+ * replaces utils.py:140-158 (timestep_embedding): out[b, i] =
+ * cos(t_b * f_i) (i < dim/2), sin(t_b * f_{i-dim/2}) (i >= dim/2),
+ * f_i = exp(-ln(max_period) * i / (dim/2)); zero column when dim is odd.
+ * t: int64[B]; out: fp32[B, dim]. */
+int vd_timestep_embedding(const int64_t* t, int B, int dim, float max_period,
+                          float* out, void* stream);
+
+/* ---- DDPM / DDIM scheduler math ----------------------------------------
+ * Tables are fp32 device arrays of length num_timesteps; t is int64[B];
+ * x tensors are [B][per_sample] in `dtype`.  z may be NULL where the
+ * formula adds no noise.
+ *
+ * q_sample: linear_noise_scheduler.py:24-46 (add_noise)
+ *   xt = sqrt_acp[t] * x0 + sqrt_1m_acp[t] * eps */
+int vd_q_sample(const void* x0, const void* eps, void* xt, const int64_t* t,
+                const float* sqrt_acp, const float* sqrt_1m_acp,
+                int64_t B, int64_t per_sample, int dtype, void* stream);
+
+/* p_sample V1: linear_noise_scheduler.py:48-76 (LinearNoiseScheduler.
+ * sample_prev_timestep).  x0 = clamp((xt - s1m[t] eps) / sqrt(acp[t])),
+ * mean = (xt - beta[t] eps / s1m[t]) / sqrt(alpha[t]); t == 0 returns mean,
+ * else mean + sqrt((1-acp[t-1])/(1-acp[t]) * beta[t]) * z. */
+int vd_p_sample_v1(const void* xt, const void* eps, const void* z,
+                   void* x_prev, void* x0, const int64_t* t,
+                   const float* betas, const float* alphas, const float* acp,
+                   const float* sqrt_1m_acp, int64_t B, int64_t per_sample,
+                   int dtype, void* stream);
+
+/* p_sample V2: linear_noise_scheduler.py:91-101 (LinearNoiseSchedulerV2).
+ * mean = xt - s1m[t] eps / sqrt(alpha[t]); sigma = sqrt((1-acp[t]) beta[t]);
+ * x_prev = mean + sigma z (also at t == 0); x0 = clamp((xt - s1m[t] eps)/sa[t]). */
+int vd_p_sample_v2(const void* xt, const void* eps, const void* z,
+                   void* x_prev, void* x0, const int64_t* t,
+                   const float* betas, const float* alphas, const float* acp,
+                   const float* sqrt_acp, const float* sqrt_1m_acp,
+                   int64_t B, int64_t per_sample, int dtype, void* stream);
+
+/* p_sample cosine: noise_scheduler.py:13-29 (CosineNoiseScheduler).
+ * mean = (xt - s1m[t] eps) / sa[t]; t > 0: x_prev = mean + sigma z with
+ * sigma = sqrt(acp[t-1] (1-acp[t]) / (1-acp[t-1])); t == 0: x_prev = mean.
+ * Second output is `mean` (the reference returns (sampled, mean)). */
+int vd_p_sample_cosine(const void* xt, const void* eps, const void* z,
+                       void* x_prev, void* mean_out, const int64_t* t,
+                       const float* acp, const float* sqrt_acp,
+                       const float* sqrt_1m_acp, int64_t B, int64_t per_sample,
+                       int dtype, void* stream);
+
+/* DDIM step (build extension, no reference oracle beyond the acp tables):
+ * x0 = (xt - sqrt(1-a_t) eps)/sqrt(a_t) [clamped to [-1,1] if clip];
+ * sigma = eta sqrt((1-a_p)/(1-a_t) (1 - a_t/a_p));
+ * x_prev = sqrt(a_p) x0 + sqrt(1-a_p-sigma^2) eps + sigma z, a_p = acp[t_prev]
+ * or 1 when t_prev < 0.  t, t_prev: int64[B]. */
+int vd_ddim_step(const void* xt, const void* eps, const void* z, void* x_prev,
+                 void* x0, const int64_t* t, const int64_t* t_prev,
+                 const float* acp, float eta, int clip, int64_t B,
+                 int64_t per_sample, int dtype, void* stream);
+
+/* ---- GroupNorm (+SiLU) -------------------------------------------------
+ * replaces GroupNorm32 (utils.py:54-56, fp32 statistics) followed by nn.SiLU
+ * (unet.py:194-198, 218-225, 297, 624-628).  x, y: [B][S][C] channels-last,
+ * S = T*H*W; gamma/beta fp32[C]; mean/rstd fp32[B*G] (saved for backward).
+ * (The ResBlock emb-add that precedes out_layers' GN is fused into the
+ * producing conv's epilogue via vd_conv3d_fwd's chan_add.) */
+size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G);
+int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta,
+                          void* y, float* mean, float* rstd, int B, int64_t S,
+                          int C, int G, float eps, int silu, int dtype,
+                          void* workspace, void* stream);
+/* dx = d/dx of silu(GN(x)); dgamma/dbeta are fp32[C] and OVERWRITTEN. */
+int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma,
+                          const float* beta, const float* mean,
+                          const float* rstd, void* dx, float* dgamma,
+                          float* dbeta, int B, int64_t S, int C, int G,
+                          int silu, int dtype, void* workspace, void* stream);
+
+/* ---- Upsample (nearest, x2 on H and W) --------------------------------
+ * replaces unet.py:112-122 F.interpolate(..., mode="nearest") with the
+ * dims=3 size (T, 2H, 2W) (and dims=2 scale_factor=2 with T=1).
+ * x: [B][T][H][W][C] -> y: [B][T][2H][2W][C]; bwd sums the 4 children. */
+int vd_upsample_nearest_hw(const void* x, void* y, int B, int T, int H, int W,
+                           int C, int dtype, void* stream);
+int vd_upsample_nearest_hw_bwd(const void* dy, void* dx, int B, int T, int H,
+                               int W, int C, int dtype, void* stream);
+
+/* ---- Convolution (implicit GEMM on MFMA) ------------------------------
+ * replaces conv_nd (utils.py:59-69) at unet.py:110,143-145,197,223,231,234,
+ * 494,627 and the 1x1 Conv1d of AttentionBlock (unet.py:298,306).
+ * Weight layouts (packed by the caller from the torch [Co][Ci][kt][kh][kw]):
+ *   fwd      : w_fwd [Co][taps][Ci]      (K = taps*Ci contiguous per Co)
+ *   bwd_data : w_bwd [Ci][taps][Co]
+ *   bwd_wgt  : dw    [Co][taps][Ci] fp32, ACCUMULATED into (zero it first)
+ * Epilogue of fwd: y = conv + bias[co] + chan_add[b][co] + residual.
+ * Any of bias / chan_add / residual may be NULL.  bias/chan_add are fp32;
+ * residual has the activation dtype and y's shape.
+ * Ci must be a multiple of 8 (bf16) or 4 (fp32); pad channels otherwise. */
+typedef struct vd_conv_desc {
+  int B;
+  int Ti, Hi, Wi, Ci;  /* input  */
+  int To, Ho, Wo, Co;  /* output */
+  int kt, kh, kw;      /* kernel taps */
+  int st, sh, sw;      /* stride */
+  int pt, ph, pw;      /* zero padding */
+  int x_cstride;       /* elements between input pixels (>= Ci), 0 = Ci */
+  int y_cstride;       /* elements between output pixels (>= Co), 0 = Co */
+  int dtype;
+} vd_conv_desc;
+
+int vd_conv3d_fwd(const vd_conv_desc* d, const void* x, const void* w_fwd,
+                  const float* bias, const float* chan_add,
+                  const void* residual, void* y, void* stream);
+/* dx[B][Ti][Hi][Wi][Ci] = conv^T(dy); overwrites dx. */
+int vd_conv3d_bwd_data(const vd_conv_desc* d, const void* dy,
+                       const void* w_bwd, void* dx, void* stream);
+/* dw[Co][taps][Ci] += sum over output pixels of dy (x) x  (fp32) */
+int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy,
+                         float* dw, void* stream);
+
+/* ---- Flash attention --------------------------------------------------
+ * replaces QKVAttentionLegacy.forward (unet.py:349-366) + the fp32 softmax
+ * (unet.py:364) and, with heads split by strides, QKVAttention (unet.py:
+ * 388-401).  One "sequence" = `seq_len` tokens of one head; sequence i
+ * starts at element (i / groups) * batch_stride + (i % groups) * group_stride
+ * of q/k/v (and of o with the o_* strides); consecutive tokens are
+ * token_stride apart.  joint: groups 1; spatial (per frame): groups T;
+ * temporal (per pixel): groups H*W, token_stride H*W*row.
+ * softmax(scale * q k^T) v, fp32 softmax statistics; lse fp32[nseq][seq_len]
+ * (natural log of the row sum of exp(scale*s)) is saved for backward. */
+typedef struct vd_attn_desc {
+  int nseq, seq_len, head_dim, groups;
+  int64_t batch_stride, group_stride, token_stride;       /* q/k/v */
+  int64_t o_batch_stride, o_group_stride, o_token_stride; /* o and dout */
+  float scale;
+  int dtype;
+} vd_attn_desc;
+
+int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k,
+                     const void* v, void* o, float* lse, void* stream);
+size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d);
+/* dout uses the o_* strides; dq/dk/dv use the q/k/v strides (so they can be
+ * written straight into a d(qkv) buffer) and are OVERWRITTEN. */
+int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k,
+                     const void* v, const void* o, const void* dout,
+                     const float* lse, void* dq, void* dk, void* dv,
+                     void* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VDIFF_H */

@@ -1,0 +1,534 @@
+// conv.hip -- channels-last 3-D convolution as implicit GEMM on MFMA (gfx950).
+//
+// Replaces conv_nd (reference utils.py:59-69) at every call site of the hot
+// path: 3x3x3 stride-1 convs (unet.py:110,197,223,231,494,627), the (1,2,2)-
+// strided Downsample conv (unet.py:143-145), 1x1x1 skip convs (unet.py:234)
+// and AttentionBlock's 1x1 Conv1d qkv / proj_out (unet.py:298,306).
+//
+//   fwd       : Y[m][n]  = sum_k A[m][k] W[n][k] (+bias[n] +chan_add[b][n] +res[m][n])
+//               m = output pixel, n = Co, k = (tap, ci), A gathered from X.
+//   bwd_data  : the same kernel in TRANSPOSED gather mode: m = input pixel,
+//               n = Ci, k = (tap, co), A gathered from dY where
+//               (pos + pad - tap) is divisible by the stride.
+//   bwd_weight: dW[co][(tap,ci)] += sum_m dY[m][co] X[src(m,tap)][ci], split-K
+//               over m with fp32 atomics; both operands are read transposed
+//               from natural [pixel][channel] LDS tiles (ds_read_b64_tr_b16).
+//
+// bf16: v_mfma_f32_16x16x32_bf16, fp32 accumulate.  fp32 (parity mode):
+// v_mfma_f32_16x16x4_f32, exact fp32 products.  Tiles are staged global ->
+// registers -> LDS (double buffered, one barrier per K step); LDS rows of
+// 64 B use a chunk XOR swizzle that is conflict-free for the fragment reads.
+#include "vd_common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kBK = 32;  // K elements per step
+
+template <typename T> struct Cfg;
+template <> struct Cfg<bf16_t> {
+  static constexpr int EPC = 8;                  // elements per 16-B chunk
+  static constexpr int CPR = kBK / EPC;          // chunks per LDS row (4)
+  static constexpr int LDK = kBK;                // LDS row length (elements)
+};
+template <> struct Cfg<float> {
+  static constexpr int EPC = 4;
+  static constexpr int CPR = kBK / EPC;          // 8
+  static constexpr int LDK = kBK + 4;            // padded rows: scalar fragment reads
+};
+
+// physical 16-B chunk of logical chunk kc in LDS row r (bf16 rows are 64 B)
+__device__ __forceinline__ int swz(int r, int kc) {
+  const int t = (r >> 2) & 3;
+  return kc ^ ((0x1320 >> (4 * t)) & 3);  // table {0,2,3,1}
+}
+
+template <typename T>
+__device__ __forceinline__ int lds_off(int r, int kc) {  // element offset of chunk (r, kc)
+  if constexpr (sizeof(T) == 2) return r * Cfg<T>::LDK + swz(r, kc) * Cfg<T>::EPC;
+  else return r * Cfg<T>::LDK + kc * Cfg<T>::EPC;
+}
+
+struct GemmGeom {
+  int B;
+  int sT, sH, sW, sC, sCs;  // gathered source: spatial, channels (K per tap), pixel stride
+  int dT, dH, dW, N, dNs;   // GEMM rows decode (output pixels), N, output pixel stride
+  int kt, kh, kw, st, sh, sw, pt, ph, pw;
+  int64_t M;
+  int K;
+};
+
+// ----------------------------------------------------------------- fwd / bwd-data
+template <typename T, int BN, bool TRANSPOSED>
+__global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(
+    GemmGeom g, const T* __restrict__ src, const T* __restrict__ wt, T* __restrict__ dst,
+    const float* __restrict__ bias, const float* __restrict__ chan_add,
+    const T* __restrict__ residual) {
+  constexpr int BM = 128;
+  constexpr int EPC = Cfg<T>::EPC, CPR = Cfg<T>::CPR, LDK = Cfg<T>::LDK;
+  constexpr int A_CH = BM * CPR / kThreads;  // A chunks per thread
+  constexpr int B_CH = BN * CPR / kThreads;
+  constexpr int WN = BN / 2;                 // wave tile: 64 x WN
+  constexpr int NI = 4, NJ = WN / 16;
+  constexpr int A_ELEMS = BM * LDK, B_ELEMS = BN * LDK;
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* lds = reinterpret_cast<T*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ntap_hw = g.kh * g.kw;
+
+  // ---- per-thread A rows (fixed for the whole K loop)
+  const int a_kc = tid % CPR;
+  int a_b[A_CH], a_t[A_CH], a_h[A_CH], a_w[A_CH];
+  bool a_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int r = tid / CPR + i * (kThreads / CPR);
+    int64_t m = m0 + r;
+    a_ok[i] = m < g.M;
+    if (!a_ok[i]) m = 0;
+    a_w[i] = (int)(m % g.dW); m /= g.dW;
+    a_h[i] = (int)(m % g.dH); m /= g.dH;
+    a_t[i] = (int)(m % g.dT);
+    a_b[i] = (int)(m / g.dT);
+  }
+  const int b_kc = tid % CPR;
+
+  auto load_tile = [&](int k0, uint4 (&ra)[A_CH], uint4 (&rb)[B_CH]) {
+    const int k = k0 + a_kc * EPC;
+    const bool kin = k < g.K;
+    const int tap = kin ? k / g.sC : 0;
+    const int c = k - tap * g.sC;
+    const int ta = tap / ntap_hw, rem = tap - ta * ntap_hw;
+    const int tb = rem / g.kw, tc = rem - tb * g.kw;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      int st_, sh_, sw_;
+      bool ok = a_ok[i] && kin;
+      if (!TRANSPOSED) {
+        st_ = a_t[i] * g.st - g.pt + ta;
+        sh_ = a_h[i] * g.sh - g.ph + tb;
+        sw_ = a_w[i] * g.sw - g.pw + tc;
+      } else {
+        const int nt = a_t[i] + g.pt - ta, nh = a_h[i] + g.ph - tb, nw = a_w[i] + g.pw - tc;
+        ok = ok && nt >= 0 && nh >= 0 && nw >= 0 && nt % g.st == 0 && nh % g.sh == 0 &&
+             nw % g.sw == 0;
+        st_ = nt / g.st;
+        sh_ = nh / g.sh;
+        sw_ = nw / g.sw;
+      }
+      ok = ok && (unsigned)st_ < (unsigned)g.sT && (unsigned)sh_ < (unsigned)g.sH &&
+           (unsigned)sw_ < (unsigned)g.sW;
+      if (ok) {
+        const int64_t pix = (((int64_t)a_b[i] * g.sT + st_) * g.sH + sh_) * g.sW + sw_;
+        ra[i] = *reinterpret_cast<const uint4*>(src + pix * g.sCs + c);
+      } else {
+        ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    const int kb = k0 + b_kc * EPC;
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int n = n0 + tid / CPR + i * (kThreads / CPR);
+      if (n < g.N && kb < g.K)
+        rb[i] = *reinterpret_cast<const uint4*>(wt + (int64_t)n * g.K + kb);
+      else
+        rb[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int stage, const uint4 (&ra)[A_CH], const uint4 (&rb)[B_CH]) {
+    T* As = lds + stage * STAGE;
+    T* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int r = tid / CPR + i * (kThreads / CPR);
+      *reinterpret_cast<uint4*>(As + lds_off<T>(r, a_kc)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int r = tid / CPR + i * (kThreads / CPR);
+      *reinterpret_cast<uint4*>(Bs + lds_off<T>(r, b_kc)) = rb[i];
+    }
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + kBK - 1) / kBK;
+  uint4 ra[A_CH], rb[B_CH];
+  load_tile(0, ra, rb);
+  store_tile(0, ra, rb);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) load_tile((kt + 1) * kBK, ra, rb);
+    const T* As = lds + (kt & 1) * STAGE;
+    const T* Bs = As + A_ELEMS;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 af[NI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + lds_off<T>(wm * 64 + 16 * i + fr, fq));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + lds_off<T>(wn * WN + 16 * j + fr, fq));
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < kBK / 4; ++s) {
+        float af[NI], bfv[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) af[i] = As[(wm * 64 + 16 * i + fr) * LDK + 4 * s + fq];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfv[j] = Bs[(wn * WN + 16 * j + fr) * LDK + 4 * s + fq];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) store_tile((kt + 1) & 1, ra, rb);
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage the fp32 tile in LDS, then coalesced 8-wide stores
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int LDC = BN + 4;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * 64 + 16 * i + fq * 4 + r) * LDC + wn * WN + 16 * j + fr] = acc[i][j][r];
+  __syncthreads();
+  const int64_t pix_per_b = (int64_t)g.dT * g.dH * g.dW;
+  const bool vec = (g.N % 8 == 0) && (g.dNs % 8 == 0);
+  for (int v = tid; v < BM * BN / 8; v += kThreads) {
+    const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+    const int64_t m = m0 + r;
+    const int n = n0 + c;
+    if (m >= g.M || n >= g.N) continue;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
+    const int bidx = (int)(m / pix_per_b);
+    const int lim = g.N - n < 8 ? g.N - n : 8;
+    if (bias)
+      for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
+    if (chan_add)
+      for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)bidx * g.N + n + e];
+    T* out = dst + m * g.dNs + n;
+    if (vec) {
+      if (residual) {
+        float rv[8];
+        load8(residual + m * g.dNs + n, rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rv[e];
+      }
+      store8(out, o);
+    } else {
+      for (int e = 0; e < lim; ++e) {
+        float val = o[e];
+        if (residual) val += Elem<T>::ld(residual + m * g.dNs + n + e);
+        Elem<T>::st(out + e, val);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------- bwd-weight
+// dW[co][tap][ci] += sum_m dY[m][co] * X[src(m, tap)][ci]
+// grid.x = co_tiles * taps * ci_tiles, grid.y = K splits over m.
+struct WgtGeom {
+  int B;
+  int Ti, Hi, Wi, Ci, xCs;  // X (gathered)
+  int To, Ho, Wo, Co, yCs;  // dY
+  int kt, kh, kw, st, sh, sw, pt, ph, pw;
+  int64_t M;                // B*To*Ho*Wo
+  int64_t m_per_split;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgtGeom g, const T* __restrict__ x,
+                                                              const T* __restrict__ dy,
+                                                              float* __restrict__ dw) {
+  constexpr int TM = 64, TN = 64;       // co x ci tile
+  constexpr int PK = 32;                // pixels per step
+  constexpr int PAD = sizeof(T) == 2 ? 8 : 4;
+  constexpr int LD = TM + PAD;          // LDS row (pixel) length, elements
+  constexpr int EPC = 16 / sizeof(T);
+  constexpr int CPRW = TM / EPC;        // 16-B chunks per 64-channel row
+  constexpr int CH = PK * CPRW / kThreads;  // chunks per thread per operand (1 bf16, 2 f32)
+  constexpr int STAGE = 2 * PK * LD;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* lds = reinterpret_cast<T*>(smem);
+
+  const int taps = g.kt * g.kh * g.kw;
+  const int co_tiles = (g.Co + TM - 1) / TM;
+  const int ci_tiles = (g.Ci + TN - 1) / TN;
+  int bid = blockIdx.x;
+  const int cot = bid % co_tiles; bid /= co_tiles;
+  const int cit = bid % ci_tiles; bid /= ci_tiles;
+  const int tap = bid;
+  const int ta = tap / (g.kh * g.kw), tb = (tap / g.kw) % g.kh, tc = tap % g.kw;
+  const int co0 = cot * TM, ci0 = cit * TN;
+  const int64_t mbeg = (int64_t)blockIdx.y * g.m_per_split;
+  int64_t mend = mbeg + g.m_per_split;
+  if (mend > g.M) mend = g.M;
+  if (mbeg >= mend) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // wave tile 32 (co) x 32 (ci)
+
+  auto load = [&](int64_t mk, uint4 (&ry)[CH], uint4 (&rx)[CH]) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int q = tid + i * kThreads;
+      const int p = q / CPRW, c = (q % CPRW) * EPC;
+      const int64_t m = mk + p;
+      ry[i] = make_uint4(0, 0, 0, 0);
+      rx[i] = make_uint4(0, 0, 0, 0);
+      if (m < mend) {
+        if (co0 + c < g.Co)
+          ry[i] = *reinterpret_cast<const uint4*>(dy + m * g.yCs + co0 + c);
+        int64_t mm = m;
+        const int w = (int)(mm % g.Wo); mm /= g.Wo;
+        const int h = (int)(mm % g.Ho); mm /= g.Ho;
+        const int t = (int)(mm % g.To);
+        const int b = (int)(mm / g.To);
+        const int s_t = t * g.st - g.pt + ta, s_h = h * g.sh - g.ph + tb, s_w = w * g.sw - g.pw + tc;
+        if ((unsigned)s_t < (unsigned)g.Ti && (unsigned)s_h < (unsigned)g.Hi &&
+            (unsigned)s_w < (unsigned)g.Wi && ci0 + c < g.Ci) {
+          const int64_t pix = (((int64_t)b * g.Ti + s_t) * g.Hi + s_h) * g.Wi + s_w;
+          rx[i] = *reinterpret_cast<const uint4*>(x + pix * g.xCs + ci0 + c);
+        }
+      }
+    }
+  };
+  auto store = [&](int stage, const uint4 (&ry)[CH], const uint4 (&rx)[CH]) {
+    T* Ys = lds + stage * STAGE;
+    T* Xs = Ys + PK * LD;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int q = tid + i * kThreads;
+      const int p = q / CPRW, c = (q % CPRW) * EPC;
+      *reinterpret_cast<uint4*>(Ys + p * LD + c) = ry[i];
+      *reinterpret_cast<uint4*>(Xs + p * LD + c) = rx[i];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (int)((mend - mbeg + PK - 1) / PK);
+  uint4 ry[CH], rx[CH];
+  load(mbeg, ry, rx);
+  store(0, ry, rx);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps;
+    if (more) load(mbeg + (int64_t)(s + 1) * PK, ry, rx);
+    const T* Ys = lds + (s & 1) * STAGE;
+    const T* Xs = Ys + PK * LD;
+    if constexpr (sizeof(T) == 2) {
+      // A[co][k=px] and B[k=px][ci] from [px][ch] tiles via transposed reads:
+      // group lane 4q+p reads row (8*fq + q [+4]), cols c0 + 4p .. +3
+      const int q4 = fr >> 2, p4 = fr & 3;
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c0 = wm * 32 + 16 * i;
+        const T* base = Ys + (8 * fq + q4) * LD + c0 + 4 * p4;
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + 4 * LD));
+        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c0 = wn * 32 + 16 * j;
+        const T* base = Xs + (8 * fq + q4) * LD + c0 + 4 * p4;
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + 4 * LD));
+        bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < PK / 4; ++kk) {
+        const int p = 4 * kk + fq;
+        float af[2], bfv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = Ys[p * LD + wm * 32 + 16 * i + fr];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfv[j] = Xs[p * LD + wn * 32 + 16 * j + fr];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) store((s + 1) & 1, ry, rx);
+    __syncthreads();
+  }
+  const int64_t krow = (int64_t)taps * g.Ci;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = ci0 + wn * 32 + 16 * j + fr;
+      if (ci >= g.Ci) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 32 + 16 * i + fq * 4 + r;
+        if (co < g.Co) atomicAdd(dw + (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[i][j][r]);
+      }
+    }
+}
+
+int check_desc(const vd_conv_desc* d) {
+  VD_REQUIRE(d, "null descriptor");
+  VD_REQUIRE(d->B > 0 && d->Ti > 0 && d->Hi > 0 && d->Wi > 0 && d->Ci > 0 && d->To > 0 &&
+                 d->Ho > 0 && d->Wo > 0 && d->Co > 0,
+             "bad conv shape");
+  VD_REQUIRE(d->kt > 0 && d->kh > 0 && d->kw > 0 && d->st > 0 && d->sh > 0 && d->sw > 0 &&
+                 d->pt >= 0 && d->ph >= 0 && d->pw >= 0,
+             "bad conv kernel/stride/pad");
+  VD_REQUIRE(d->Ci % 8 == 0, "Ci=%d must be a multiple of 8 (pad channels)", d->Ci);
+  VD_REQUIRE(d->To == (d->Ti + 2 * d->pt - d->kt) / d->st + 1 &&
+                 d->Ho == (d->Hi + 2 * d->ph - d->kh) / d->sh + 1 &&
+                 d->Wo == (d->Wi + 2 * d->pw - d->kw) / d->sw + 1,
+             "output shape does not match input/kernel/stride/pad");
+  VD_REQUIRE(d->x_cstride == 0 || (d->x_cstride >= d->Ci && d->x_cstride % 8 == 0),
+             "bad x_cstride");
+  VD_REQUIRE(d->y_cstride == 0 || d->y_cstride >= d->Co, "bad y_cstride");
+  return VD_OK;
+}
+
+template <typename T, bool TR>
+int launch_gemm(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
+                const float* ca, const void* res, hipStream_t st) {
+  const int64_t mt = vd_cdiv(g.M, 128);
+  const bool narrow = g.N <= 64;
+  if (narrow) {
+    constexpr int BN = 64;
+    const size_t lds_ab = 2 * (128 + BN) * Cfg<T>::LDK * sizeof(T);
+    const size_t lds_c = 128 * (BN + 4) * sizeof(float);
+    dim3 grid((unsigned)mt, (unsigned)vd_cdiv(g.N, BN));
+    conv_gemm_kernel<T, BN, TR><<<grid, kThreads, lds_ab > lds_c ? lds_ab : lds_c, st>>>(
+        g, (const T*)src, (const T*)wt, (T*)dst, bias, ca, (const T*)res);
+  } else {
+    constexpr int BN = 128;
+    const size_t lds_ab = 2 * (128 + BN) * Cfg<T>::LDK * sizeof(T);
+    const size_t lds_c = 128 * (BN + 4) * sizeof(float);
+    dim3 grid((unsigned)mt, (unsigned)vd_cdiv(g.N, BN));
+    conv_gemm_kernel<T, BN, TR><<<grid, kThreads, lds_ab > lds_c ? lds_ab : lds_c, st>>>(
+        g, (const T*)src, (const T*)wt, (T*)dst, bias, ca, (const T*)res);
+  }
+  return VD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vd_conv3d_fwd(const vd_conv_desc* d, const void* x, const void* w_fwd, const float* bias,
+                  const float* chan_add, const void* residual, void* y, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  VD_REQUIRE(x && w_fwd && y, "null tensor");
+  GemmGeom g;
+  g.B = d->B;
+  g.sT = d->Ti; g.sH = d->Hi; g.sW = d->Wi; g.sC = d->Ci;
+  g.sCs = d->x_cstride ? d->x_cstride : d->Ci;
+  g.dT = d->To; g.dH = d->Ho; g.dW = d->Wo; g.N = d->Co;
+  g.dNs = d->y_cstride ? d->y_cstride : d->Co;
+  g.kt = d->kt; g.kh = d->kh; g.kw = d->kw;
+  g.st = d->st; g.sh = d->sh; g.sw = d->sw;
+  g.pt = d->pt; g.ph = d->ph; g.pw = d->pw;
+  g.M = (int64_t)d->B * d->To * d->Ho * d->Wo;
+  g.K = d->kt * d->kh * d->kw * d->Ci;
+  return VD_DISPATCH_DTYPE(d->dtype, T, {
+    launch_gemm<T, false>(g, x, w_fwd, y, bias, chan_add, residual, VD_STREAM(stream));
+  });
+}
+
+int vd_conv3d_bwd_data(const vd_conv_desc* d, const void* dy, const void* w_bwd, void* dx,
+                       void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  VD_REQUIRE(dy && w_bwd && dx, "null tensor");
+  VD_REQUIRE(d->Co % 8 == 0, "bwd_data needs Co %% 8 == 0 (got %d)", d->Co);
+  VD_REQUIRE(d->y_cstride == 0 || d->y_cstride % 8 == 0, "bad y_cstride");
+  GemmGeom g;
+  g.B = d->B;
+  g.sT = d->To; g.sH = d->Ho; g.sW = d->Wo; g.sC = d->Co;
+  g.sCs = d->y_cstride ? d->y_cstride : d->Co;
+  g.dT = d->Ti; g.dH = d->Hi; g.dW = d->Wi; g.N = d->Ci;
+  g.dNs = d->x_cstride ? d->x_cstride : d->Ci;
+  g.kt = d->kt; g.kh = d->kh; g.kw = d->kw;
+  g.st = d->st; g.sh = d->sh; g.sw = d->sw;
+  g.pt = d->pt; g.ph = d->ph; g.pw = d->pw;
+  g.M = (int64_t)d->B * d->Ti * d->Hi * d->Wi;
+  g.K = d->kt * d->kh * d->kw * d->Co;
+  return VD_DISPATCH_DTYPE(d->dtype, T, {
+    launch_gemm<T, true>(g, dy, w_bwd, dx, nullptr, nullptr, nullptr, VD_STREAM(stream));
+  });
+}
+
+int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, float* dw,
+                         void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  VD_REQUIRE(x && dy && dw, "null tensor");
+  VD_REQUIRE(d->Co % 8 == 0, "bwd_weight needs Co %% 8 == 0 (got %d)", d->Co);
+  WgtGeom g;
+  g.B = d->B;
+  g.Ti = d->Ti; g.Hi = d->Hi; g.Wi = d->Wi; g.Ci = d->Ci;
+  g.xCs = d->x_cstride ? d->x_cstride : d->Ci;
+  g.To = d->To; g.Ho = d->Ho; g.Wo = d->Wo; g.Co = d->Co;
+  g.yCs = d->y_cstride ? d->y_cstride : d->Co;
+  g.kt = d->kt; g.kh = d->kh; g.kw = d->kw;
+  g.st = d->st; g.sh = d->sh; g.sw = d->sw;
+  g.pt = d->pt; g.ph = d->ph; g.pw = d->pw;
+  g.M = (int64_t)d->B * d->To * d->Ho * d->Wo;
+  const int taps = d->kt * d->kh * d->kw;
+  const int64_t tiles = (int64_t)vd_cdiv(d->Co, 64) * vd_cdiv(d->Ci, 64) * taps;
+  // split the pixel reduction so the grid has ~2048 workgroups, >= 512 px each
+  int64_t splits = vd_cdiv(2048, tiles);
+  int64_t maxs = vd_cdiv(g.M, 512);
+  if (splits > maxs) splits = maxs;
+  if (splits < 1) splits = 1;
+  g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 32) * 32;
+  splits = vd_cdiv(g.M, g.m_per_split);
+  return VD_DISPATCH_DTYPE(d->dtype, T, {
+    constexpr int LD = 64 + (sizeof(T) == 2 ? 8 : 4);
+    const size_t lds = 2 * 2 * 32 * LD * sizeof(T);
+    conv_wgrad_kernel<T><<<dim3((unsigned)tiles, (unsigned)splits), kThreads, lds,
+                           VD_STREAM(stream)>>>(g, (const T*)x, (const T*)dy, dw);
+  });
+}
+
+}  // extern "C"

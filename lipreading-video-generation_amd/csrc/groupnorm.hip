@@ -1,0 +1,403 @@
+// groupnorm.hip -- fused GroupNorm(32) + SiLU, forward and backward, on
+// channels-last activations [B][S][C] (S = T*H*W).
+//
+// Replaces GroupNorm32 (reference utils.py:54-56: fp32 statistics, eps 1e-5,
+// affine) + nn.SiLU (unet.py:194-198, 218-225, 624-628) and the bare GN of
+// AttentionBlock (unet.py:297, silu = 0).
+//
+// HBM traffic (the bound): fwd = 2 reads + 1 write of x; bwd = 2 reads of x
+// and dy + 1 write of dx.  Statistics are fp32 and combined with Chan's
+// parallel formula (per-thread shifted sums -> per-chunk -> per-sample), so
+// the variance does not cancel when |mean| >> std.
+#include "vd_common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kVec = 8;             // channels per lane
+constexpr int kTargetChunks = 2048; // workgroups per launch (B * nchunk)
+
+struct GNPlan {
+  int rows_per_iter;  // pixel rows a WG covers per iteration
+  int64_t chunk_px;   // pixels per WG
+  int nchunk;         // chunks per sample
+};
+
+inline GNPlan gn_plan(int B, int64_t S, int C) {
+  GNPlan p;
+  const int nvec = C / kVec;
+  p.rows_per_iter = kThreads / nvec;
+  if (p.rows_per_iter < 1) p.rows_per_iter = 1;
+  int64_t want = vd_cdiv(S * B, kTargetChunks);
+  if (want < p.rows_per_iter) want = p.rows_per_iter;
+  want = vd_cdiv(want, p.rows_per_iter) * p.rows_per_iter;
+  p.chunk_px = want;
+  p.nchunk = (int)vd_cdiv(S, want);
+  return p;
+}
+
+struct Stat {  // count, mean, M2
+  float n, m, q;
+};
+__device__ __forceinline__ Stat chan(Stat a, Stat b) {
+  const float n = a.n + b.n;
+  if (n == 0.f) return a;
+  const float d = b.m - a.m;
+  const float fb = b.n / n;
+  Stat r;
+  r.n = n;
+  r.m = a.m + d * fb;
+  r.q = a.q + b.q + d * d * a.n * fb;
+  return r;
+}
+
+// ---------------------------------------------------------------- forward
+// grid (nchunk, B).  Per WG: per-group (n, mean, M2) over its chunk.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void gn_stats_kernel(const T* __restrict__ x, int64_t S,
+                                                            int C, int G, int64_t chunk_px,
+                                                            int rows_per_iter,
+                                                            float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Stat* sh = reinterpret_cast<Stat*>(smem);  // [rows_per_iter][C]
+  const int nvec = C / kVec;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int r = tid / nvec, cv = tid % nvec;
+  const int64_t p0 = (int64_t)blockIdx.x * chunk_px;
+  int64_t p1 = p0 + chunk_px;
+  if (p1 > S) p1 = S;
+  const T* xb = x + (int64_t)b * S * C;
+  const bool active = r < rows_per_iter;
+  float shift[kVec], s1[kVec], s2[kVec];
+  float cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < kVec; ++j) s1[j] = s2[j] = shift[j] = 0.f;
+  if (active && p0 + r < p1) load8(xb + (p0 + r) * C + cv * kVec, shift);
+  if (active) {
+    for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
+      float v[kVec];
+      load8(xb + p * C + cv * kVec, v);
+#pragma unroll
+      for (int j = 0; j < kVec; ++j) {
+        const float d = v[j] - shift[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+      cnt += 1.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+      Stat s;
+      s.n = cnt;
+      s.m = cnt > 0.f ? shift[j] + s1[j] / cnt : 0.f;
+      s.q = cnt > 0.f ? fmaxf(s2[j] - s1[j] * s1[j] / cnt, 0.f) : 0.f;
+      sh[r * C + cv * kVec + j] = s;
+    }
+  }
+  __syncthreads();
+  // one thread per channel: combine rows
+  for (int c = tid; c < C; c += kThreads) {
+    Stat a = sh[c];
+    for (int rr = 1; rr < rows_per_iter; ++rr) a = chan(a, sh[rr * C + c]);
+    sh[c] = a;
+  }
+  __syncthreads();
+  const int cpg = C / G;
+  for (int g = tid; g < G; g += kThreads) {
+    Stat a = sh[g * cpg];
+    for (int k = 1; k < cpg; ++k) a = chan(a, sh[g * cpg + k]);
+    float* o = part + (((int64_t)b * gridDim.x + blockIdx.x) * G + g) * 3;
+    o[0] = a.n;
+    o[1] = a.m;
+    o[2] = a.q;
+  }
+}
+
+// grid B, 256 threads: combine nchunk partials per group -> mean, rstd
+__global__ __launch_bounds__(kThreads) void gn_finalize_kernel(const float* __restrict__ part,
+                                                               int nchunk, int G, float eps,
+                                                               float* __restrict__ mean,
+                                                               float* __restrict__ rstd) {
+  __shared__ Stat sh[kThreads];
+  const int b = blockIdx.x;
+  const int per_g = kThreads / G;  // threads per group (G <= 256)
+  const int g = threadIdx.x / per_g, lane = threadIdx.x % per_g;
+  Stat a{0.f, 0.f, 0.f};
+  if (g < G) {
+    for (int k = lane; k < nchunk; k += per_g) {
+      const float* p = part + (((int64_t)b * nchunk + k) * G + g) * 3;
+      a = chan(a, Stat{p[0], p[1], p[2]});
+    }
+  }
+  sh[threadIdx.x] = a;
+  __syncthreads();
+  if (g < G && lane == 0) {
+    Stat t = sh[threadIdx.x];
+    for (int k = 1; k < per_g; ++k) t = chan(t, sh[threadIdx.x + k]);
+    const float var = t.n > 0.f ? t.q / t.n : 0.f;  // biased, as torch GroupNorm
+    mean[b * G + g] = t.m;
+    rstd[b * G + g] = rsqrtf(var + eps);
+  }
+}
+
+template <typename T, bool SILU>
+__global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict__ x,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            T* __restrict__ y, int B, int64_t S,
+                                                            int C, int G) {
+  const int nvec = C / kVec;
+  const int cpg = C / G;
+  const int64_t n = (int64_t)B * S * nvec;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % nvec) * kVec;
+    const int b = (int)(i / ((int64_t)S * nvec));
+    float v[kVec];
+    load8(x + i * kVec, v);
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+      const int c = c0 + j;
+      const int g = b * G + c / cpg;
+      const float sc = gamma[c] * rstd[g];
+      const float z = (v[j] - mean[g]) * sc + beta[c];
+      v[j] = SILU ? silu_f(z) : z;
+    }
+    store8(y + i * kVec, v);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// grid (nchunk, B): per-channel partial sums A = sum dz, Bs = sum dz * xhat
+template <typename T, bool SILU>
+__global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
+    int64_t S, int C, int G, int64_t chunk_px, int rows_per_iter, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* sh = reinterpret_cast<float2*>(smem);  // [rows_per_iter][C]
+  const int nvec = C / kVec;
+  const int cpg = C / G;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int r = tid / nvec, cv = tid % nvec;
+  const int64_t p0 = (int64_t)blockIdx.x * chunk_px;
+  int64_t p1 = p0 + chunk_px;
+  if (p1 > S) p1 = S;
+  const T* xb = x + (int64_t)b * S * C;
+  const T* db = dy + (int64_t)b * S * C;
+  float mu[kVec], rs[kVec], ga[kVec], be[kVec], sa[kVec], sb[kVec];
+  if (r < rows_per_iter) {
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+      const int c = cv * kVec + j;
+      mu[j] = mean[b * G + c / cpg];
+      rs[j] = rstd[b * G + c / cpg];
+      ga[j] = gamma[c];
+      be[j] = beta[c];
+      sa[j] = sb[j] = 0.f;
+    }
+    for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
+      float v[kVec], d[kVec];
+      load8(xb + p * C + cv * kVec, v);
+      load8(db + p * C + cv * kVec, d);
+#pragma unroll
+      for (int j = 0; j < kVec; ++j) {
+        const float xh = (v[j] - mu[j]) * rs[j];
+        float dz = d[j];
+        if (SILU) {
+          const float z = xh * ga[j] + be[j];
+          const float sg = 1.f / (1.f + __expf(-z));
+          dz *= sg * (1.f + z * (1.f - sg));
+        }
+        sa[j] += dz;
+        sb[j] += dz * xh;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) sh[r * C + cv * kVec + j] = make_float2(sa[j], sb[j]);
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kThreads) {
+    float2 a = sh[c];
+    for (int rr = 1; rr < rows_per_iter; ++rr) {
+      a.x += sh[rr * C + c].x;
+      a.y += sh[rr * C + c].y;
+    }
+    float* o = part + (((int64_t)b * gridDim.x + blockIdx.x) * C + c) * 2;
+    o[0] = a.x;
+    o[1] = a.y;
+  }
+}
+
+// one WG, one thread per channel: per-sample sums, group coefficients, dgamma/dbeta
+__global__ void gn_bwd_finalize_kernel(const float* __restrict__ part, int B, int nchunk, int C,
+                                       int G, int64_t S, const float* __restrict__ gamma,
+                                       float* __restrict__ coef, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sA = reinterpret_cast<float*>(smem);  // [C] gamma * A
+  float* sB = sA + C;                          // [C] gamma * B
+  const int cpg = C / G;
+  const float inv_n = 1.f / ((float)cpg * (float)S);
+  float dg[4] = {0, 0, 0, 0}, db[4] = {0, 0, 0, 0};  // up to 4 channels per thread
+  for (int b = 0; b < B; ++b) {
+    int slot = 0;
+    for (int c = threadIdx.x; c < C; c += blockDim.x, ++slot) {
+      float a = 0.f, s = 0.f;
+      for (int k = 0; k < nchunk; ++k) {
+        const float* p = part + (((int64_t)b * nchunk + k) * C + c) * 2;
+        a += p[0];
+        s += p[1];
+      }
+      db[slot] += a;
+      dg[slot] += s;
+      sA[c] = gamma[c] * a;
+      sB[c] = gamma[c] * s;
+    }
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+      float a = 0.f, s = 0.f;
+      for (int k = 0; k < cpg; ++k) {
+        a += sA[g * cpg + k];
+        s += sB[g * cpg + k];
+      }
+      coef[(b * G + g) * 2 + 0] = a * inv_n;
+      coef[(b * G + g) * 2 + 1] = s * inv_n;
+    }
+    __syncthreads();
+  }
+  int slot = 0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x, ++slot) {
+    dgamma[c] = dg[slot];
+    dbeta[c] = db[slot];
+  }
+}
+
+template <typename T, bool SILU>
+__global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ coef, T* __restrict__ dx, int B, int64_t S, int C, int G) {
+  const int nvec = C / kVec;
+  const int cpg = C / G;
+  const int64_t n = (int64_t)B * S * nvec;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % nvec) * kVec;
+    const int b = (int)(i / ((int64_t)S * nvec));
+    float v[kVec], d[kVec];
+    load8(x + i * kVec, v);
+    load8(dy + i * kVec, d);
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+      const int c = c0 + j;
+      const int g = b * G + c / cpg;
+      const float rs = rstd[g];
+      const float xh = (v[j] - mean[g]) * rs;
+      float dz = d[j];
+      if (SILU) {
+        const float z = xh * gamma[c] + beta[c];
+        const float sg = 1.f / (1.f + __expf(-z));
+        dz *= sg * (1.f + z * (1.f - sg));
+      }
+      v[j] = rs * (gamma[c] * dz - coef[2 * g] - xh * coef[2 * g + 1]);
+    }
+    store8(dx + i * kVec, v);
+  }
+}
+
+inline int apply_grid(int64_t nvec_total) {
+  int64_t g = vd_cdiv(nvec_total, kThreads);
+  return (int)(g < 256 * 16 ? (g > 0 ? g : 1) : 256 * 16);
+}
+
+int gn_check(const void* x, int B, int64_t S, int C, int G) {
+  VD_REQUIRE(x, "null tensor");
+  VD_REQUIRE(B > 0 && S > 0 && C > 0 && G > 0, "bad shape B=%d S=%lld C=%d G=%d", B,
+             (long long)S, C, G);
+  VD_REQUIRE(C % G == 0, "C=%d not divisible by groups=%d", C, G);
+  VD_REQUIRE(C % kVec == 0, "C=%d must be a multiple of %d", C, kVec);
+  VD_REQUIRE(C / kVec <= kThreads, "C=%d too large", C);
+  VD_REQUIRE(G <= kThreads, "G=%d too large", G);
+  VD_REQUIRE(C <= 4 * kThreads, "C=%d too large for bwd finalize", C);
+  return VD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G) {
+  if (B <= 0 || S <= 0 || C <= 0 || G <= 0 || C % kVec) return 0;
+  GNPlan p = gn_plan(B, S, C);
+  size_t fwd = (size_t)B * p.nchunk * G * 3 * sizeof(float);
+  size_t bwd = ((size_t)B * p.nchunk * C * 2 + (size_t)B * G * 2) * sizeof(float);
+  return (fwd > bwd ? fwd : bwd) + 256;
+}
+
+int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, void* y,
+                          float* mean, float* rstd, int B, int64_t S, int C, int G, float eps,
+                          int silu, int dtype, void* workspace, void* stream) {
+  int rc = gn_check(x, B, S, C, G);
+  if (rc) return rc;
+  VD_REQUIRE(gamma && beta && y && mean && rstd && workspace, "null argument");
+  GNPlan p = gn_plan(B, S, C);
+  float* part = reinterpret_cast<float*>(workspace);
+  hipStream_t st = VD_STREAM(stream);
+  const size_t lds = (size_t)p.rows_per_iter * C * sizeof(Stat);
+  return VD_DISPATCH_DTYPE(dtype, T, {
+    gn_stats_kernel<T><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
+        (const T*)x, S, C, G, p.chunk_px, p.rows_per_iter, part);
+    gn_finalize_kernel<<<B, kThreads, 0, st>>>(part, p.nchunk, G, eps, mean, rstd);
+    const int grid = apply_grid((int64_t)B * S * (C / kVec));
+    if (silu)
+      gn_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
+                                                          (T*)y, B, S, C, G);
+    else
+      gn_apply_kernel<T, false><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
+                                                           (T*)y, B, S, C, G);
+  });
+}
+
+int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, const float* beta,
+                          const float* mean, const float* rstd, void* dx, float* dgamma,
+                          float* dbeta, int B, int64_t S, int C, int G, int silu, int dtype,
+                          void* workspace, void* stream) {
+  int rc = gn_check(x, B, S, C, G);
+  if (rc) return rc;
+  VD_REQUIRE(dy && gamma && beta && mean && rstd && dx && dgamma && dbeta && workspace,
+             "null argument");
+  GNPlan p = gn_plan(B, S, C);
+  float* part = reinterpret_cast<float*>(workspace);
+  float* coef = part + (size_t)B * p.nchunk * C * 2;
+  hipStream_t st = VD_STREAM(stream);
+  const size_t lds = (size_t)p.rows_per_iter * C * sizeof(float2);
+  const int grid = apply_grid((int64_t)B * S * (C / kVec));
+  return VD_DISPATCH_DTYPE(dtype, T, {
+    if (silu)
+      gn_bwd_reduce_kernel<T, true><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
+          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
+          p.rows_per_iter, part);
+    else
+      gn_bwd_reduce_kernel<T, false><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
+          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
+          p.rows_per_iter, part);
+    gn_bwd_finalize_kernel<<<1, kThreads, 2 * C * sizeof(float), st>>>(part, B, p.nchunk, C, G,
+                                                                       S, gamma, coef, dgamma,
+                                                                       dbeta);
+    if (silu)
+      gn_bwd_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, (const T*)dy, gamma,
+                                                              beta, mean, rstd, coef, (T*)dx, B,
+                                                              S, C, G);
+    else
+      gn_bwd_apply_kernel<T, false><<<grid, kThreads, 0, st>>>((const T*)x, (const T*)dy, gamma,
+                                                               beta, mean, rstd, coef, (T*)dx,
+                                                               B, S, C, G);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// vd_common.h -- shared device/host helpers for libvdiff (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/vdiff.h"
+
+// ---------------------------------------------------------------- errors
+namespace vd {
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace vd
+
+#define VD_REQUIRE(cond, ...)                                   \
+  do {                                                          \
+    if (!(cond)) return vd::fail(VD_EINVAL, __VA_ARGS__);       \
+  } while (0)
+
+#define VD_STREAM(s) (reinterpret_cast<hipStream_t>(s))
+
+// ---------------------------------------------------------------- types
+typedef uint16_t bf16_t;  // raw bf16 storage
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+// round-to-nearest-even; NaN stays NaN (quiet bit forced)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// Load/store N consecutive elements of T as fp32 (N*sizeof(T) must be 8 or 16 B aligned).
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static constexpr int kDtype = VD_F32;
+  __device__ __forceinline__ static float ld(const float* p) { return *p; }
+  __device__ __forceinline__ static void st(float* p, float v) { *p = v; }
+};
+template <> struct Elem<bf16_t> {
+  static constexpr int kDtype = VD_BF16;
+  __device__ __forceinline__ static float ld(const bf16_t* p) { return bf2f(*p); }
+  __device__ __forceinline__ static void st(bf16_t* p, float v) { *p = f2bf(v); }
+};
+
+// 8 elements <-> 8 floats, vectorised (bf16: one 16-B access, f32: two).
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+  uint4 r = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ float silu_f(float z) { return z / (1.0f + __expf(-z)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// dispatch on the runtime dtype tag
+#define VD_DISPATCH_DTYPE(dtype, T, ...)                               \
+  [&]() -> int {                                                       \
+    if ((dtype) == VD_F32) { using T = float; __VA_ARGS__; }           \
+    else if ((dtype) == VD_BF16) { using T = bf16_t; __VA_ARGS__; }    \
+    else return vd::fail(VD_EUNSUPPORTED, "unknown dtype %d", (int)(dtype)); \
+    return vd::check_launch(__func__);                                 \
+  }()
+
+static inline int64_t vd_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

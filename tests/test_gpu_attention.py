@@ -1,0 +1,76 @@
+"""Flash attention (fwd + bwd) vs the oracle's materialised softmax attention and the
+reference golden vectors.  Modes: joint (reference), spatial, temporal."""
+import pytest
+import torch
+
+from oracle import nn as onn
+from oracle.fixtures import rel_l2, seeded
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _check(B, C, heads, T, HW, mode, legacy, dtype, seed):
+    from vdiff import ops
+    N = T * HW
+    qkv = seeded((B, 3 * C, N), seed)
+    if dtype == torch.bfloat16:
+        qkv = qkv.bfloat16().float()
+    qr = qkv.clone().requires_grad_(True)
+    ref = onn.qkv_attention(qr, heads, legacy=legacy, mode=mode, spatial=(T, HW, 1))
+    g = seeded(ref.shape, seed + 1)
+    ref.backward(g)
+    qd = ops.to_cl(qkv.to(dev, dtype)).requires_grad_(True)
+    out = ops.attention(qd, heads=heads, mode=mode, spatial=(T, HW, 1), legacy=legacy)
+    out.backward(ops.to_cl(g.to(dev, dtype)))
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    e_out, e_grad = rel_l2(out, ref), rel_l2(qd.grad, qr.grad)
+    assert e_out < tol, (e_out, e_grad)
+    assert e_grad < 2 * tol, (e_out, e_grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [32, 64, 128, 256])
+def test_joint_head_dims(C, dtype):
+    _check(2, C, 1, 3, 67, "joint", True, dtype, 10 + C)  # N = 201: ragged tiles
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode", ["spatial", "temporal"])
+def test_spatial_temporal(mode, dtype):
+    _check(2, 64, 1, 5, 130, mode, True, dtype, 20)
+
+
+@pytest.mark.parametrize("legacy", [True, False])
+def test_multi_head_orders(legacy):
+    _check(2, 128, 2, 1, 300, "joint", legacy, torch.float32, 30)
+    _check(1, 128, 4, 2, 64, "temporal", legacy, torch.float32, 31)
+
+
+def test_single_token_and_long_sequence():
+    _check(1, 64, 1, 1, 1, "joint", True, torch.float32, 40)
+    _check(1, 64, 1, 1, 4096, "joint", True, torch.bfloat16, 41)
+
+
+def test_scores_with_large_logits():
+    """Large |q.k| forces the online-softmax rescale branch on many tiles."""
+    from vdiff import ops
+    B, C, N = 1, 64, 777
+    qkv = seeded((B, 3 * C, N), 50) * 4.0
+    qkv[:, :C, 500] *= 8  # one query row with a far larger max late in the sequence
+    ref = onn.qkv_attention(qkv, 1)
+    out = ops.attention(ops.to_cl(qkv.to(dev)), heads=1)
+    assert rel_l2(out, ref) < 2e-5
+
+
+def test_golden_regroupings():
+    from vdiff import ops
+    g = golden("blocks.npz")
+    B, C, T, HW = 2, 64, 3, 36
+    qkv = ops.to_cl(seeded((B, 3 * C, T * HW), 46).to(dev))
+    for mode, key in (("joint", "st_joint"), ("spatial", "st_spatial"),
+                      ("temporal", "st_temporal")):
+        out = ops.attention(qkv, heads=1, mode=mode, spatial=(T, 6, 6))
+        assert rel_l2(out, g[key]) < 2e-5, mode

@@ -1,0 +1,88 @@
+"""Implicit-GEMM conv kernels (fwd, bwd-data, bwd-weight) vs the oracle (torch CPU conv)."""
+import pytest
+import torch
+
+from oracle import nn as onn
+from oracle.fixtures import rel_l2, seeded
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+CASES = [
+    # (x shape, Co, kernel, stride, padding)
+    ((2, 64, 3, 9, 11), 64, 3, 1, 1),
+    ((1, 195, 2, 8, 8), 64, 3, 1, 1),          # unpadded input channels (UNetAudio concat)
+    ((2, 64, 2, 6, 7), 3, 3, 1, 1),            # model out conv: Co = 3
+    ((1, 64, 2, 9, 9), 64, 3, (1, 2, 2), 1),   # Downsample
+    ((2, 64, 2, 5, 5), 128, 1, 1, 0),          # ResBlock skip
+    ((1, 384, 2, 4, 4), 256, 1, 1, 0),
+    ((1, 512, 2, 4, 6), 256, 3, 1, 1),         # N > 128: two column tiles
+    ((2, 64, 200), 192, 1, 1, 0),              # AttentionBlock qkv (Conv1d)
+    ((2, 64, 10, 10), 64, 3, 1, 1),            # dims = 2
+    ((1, 32, 4, 16, 16), 32, 3, 1, 1),
+]
+
+
+def _weights(Ci, Co, k, nd, seed):
+    ks = (k,) * nd if isinstance(k, int) else k
+    w = seeded((Co, Ci) + ks, seed) / (Ci * (k ** nd if isinstance(k, int) else 1)) ** 0.5
+    b = 0.1 * seeded((Co,), seed + 1)
+    return w, b
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_conv_fwd_bwd_vs_oracle(case, dtype):
+    from vdiff import ops
+    shape, Co, k, stride, pad = CASES[case]
+    nd = len(shape) - 2
+    Ci = shape[1]
+    x = seeded(shape, 100 + case)
+    w, b = _weights(Ci, Co, k, nd, 200 + case)
+    if dtype == torch.bfloat16:  # oracle sees the same rounded operands
+        x = x.bfloat16().float()
+        w = w.bfloat16().float()
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = onn.conv(xr, wr, br, stride=stride, padding=pad)
+    g = seeded(yr.shape, 300 + case)
+    yr.backward(g)
+
+    xd = ops.to_cl(x.to(dev, dtype)).requires_grad_(True)
+    wd = w.to(dev).requires_grad_(True)
+    bd = b.to(dev).requires_grad_(True)
+    y = ops.conv(xd, wd, bd, stride=stride, padding=pad)
+    assert list(y.shape) == list(yr.shape)
+    assert ops.is_cl(y)
+    y.backward(ops.to_cl(g.to(dev, dtype)))
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    assert rel_l2(y, yr) < tol, rel_l2(y, yr)
+    assert rel_l2(xd.grad, xr.grad) < tol * 2, rel_l2(xd.grad, xr.grad)
+    assert rel_l2(wd.grad, wr.grad) < tol * 2, rel_l2(wd.grad, wr.grad)
+    assert rel_l2(bd.grad, br.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_fused_epilogue(dtype):
+    """y = conv(x) + bias + chan_add[b, co] + residual (the ResBlock emb-add and skip-add)."""
+    from vdiff import ops
+    x = seeded((2, 64, 2, 7, 9), 1)
+    w, b = _weights(64, 128, 3, 3, 2)
+    ca = seeded((2, 128), 4)
+    res = seeded((2, 128, 2, 7, 9), 5)
+    if dtype == torch.bfloat16:
+        x, w, res = x.bfloat16().float(), w.bfloat16().float(), res.bfloat16().float()
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b, ca, res)]
+    yr = onn.conv(leaves[0], leaves[1], leaves[2], padding=1) + leaves[3][:, :, None, None, None] \
+        + leaves[4]
+    g = seeded(yr.shape, 6)
+    yr.backward(g)
+    dl = [x.to(dev, dtype), w.to(dev), b.to(dev), ca.to(dev), res.to(dev, dtype)]
+    dl[0] = ops.to_cl(dl[0])
+    dl[4] = ops.to_cl(dl[4])
+    dl = [t.requires_grad_(True) for t in dl]
+    y = ops.conv(dl[0], dl[1], dl[2], padding=1, chan_add=dl[3], residual=dl[4])
+    y.backward(ops.to_cl(g.to(dev, dtype)))
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    assert rel_l2(y, yr) < tol
+    for a, r in zip(dl, leaves):
+        assert rel_l2(a.grad, r.grad) < 2 * tol + 1e-5

@@ -1,0 +1,66 @@
+"""Fused GroupNorm(+SiLU) HIP kernels vs the reference golden vectors and the oracle."""
+import pytest
+import torch
+
+from oracle import nn as onn
+from oracle.fixtures import rel_l2, seeded
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _run(x, w, b, silu, dtype, g):
+    from vdiff import ops
+    xd = ops.to_cl(x.to(dev, dtype)).requires_grad_(True)
+    wd = w.to(dev).clone().requires_grad_(True)
+    bd = b.to(dev).clone().requires_grad_(True)
+    y = ops.group_norm_silu(xd, wd, bd, 32, 1e-5, silu)
+    y.backward(ops.to_cl(g.to(dev, dtype)))
+    return y.float().cpu(), xd.grad.float().cpu(), wd.grad.cpu(), bd.grad.cpu()
+
+
+def test_gn_silu_golden_fp32():
+    gg = golden("blocks.npz")
+    x = seeded((2, 64, 2, 6, 6), 20)
+    g = seeded(x.shape, 22)
+    y, dx, dw, db = _run(x, gg["gn_w"], gg["gn_b"], True, torch.float32, g)
+    torch.testing.assert_close(y, gg["gn_y"], atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(dx, gg["gn_dx"], atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(dw, gg["gn_dw"], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(db, gg["gn_db"], atol=1e-4, rtol=1e-4)
+
+
+def test_gn_plain_golden_fp32_offset_mean():
+    gg = golden("blocks.npz")
+    x = seeded((2, 128, 40), 23) * 3 + 1.5
+    g = seeded(x.shape, 25)
+    y, dx, dw, db = _run(x, gg["gn2_w"], gg["gn2_b"], False, torch.float32, g)
+    torch.testing.assert_close(y, gg["gn2_y"], atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(dx, gg["gn2_dx"], atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(dw, gg["gn2_dw"], atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("C,shape", [(64, (1, 64, 16, 128, 128)), (192, (2, 192, 3, 9, 11)),
+                                     (384, (1, 384, 2, 8, 8)), (512, (2, 512, 1, 4, 4)),
+                                     (256, (3, 256, 16, 32, 32))])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gn_silu_vs_oracle_shapes(C, shape, dtype):
+    x = seeded(shape, 3) * 2 + 10.0  # |mean| >> std: exercises the Chan combine
+    w = 1 + 0.1 * seeded((C,), 4)
+    b = 0.1 * seeded((C,), 5)
+    g = seeded(shape, 6)
+    xr = x.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = onn.group_norm(xr, wr, br, silu=True)
+    yr.backward(g)
+    if dtype == torch.bfloat16:  # compare to the oracle fed the same rounded input
+        x = x.to(dtype).float()
+    y, dx, dw, db = _run(x, w, b, True, dtype, g)
+    tol_y = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_l2(y, yr) < tol_y * 3
+    if dtype == torch.float32:
+        assert rel_l2(dx, xr.grad) < 1e-4
+        assert rel_l2(dw, wr.grad) < 1e-4
+        assert rel_l2(db, br.grad) < 1e-4

@@ -1,0 +1,176 @@
+"""Pin the oracle (CPU restatement) to the golden vectors made by importing the
+reference (tests/golden/gen_golden.py).  CPU only."""
+import torch
+import torch.nn.functional as F
+
+from oracle import nn as onn
+from oracle import schedulers as osch
+from oracle.fixtures import FULL2D, FULL2D_SHAPE, TINY3D, TINY3D_SHAPE, rel_l2, seeded
+from oracle.unet import (audio_conditioned_input, audio_param_shapes, build_plan, init_params,
+                         param_shapes, unet_forward)
+
+from conftest import golden
+
+
+def close(a, b, atol=1e-5, rtol=1e-5):
+    torch.testing.assert_close(a.float(), b.float(), atol=atol, rtol=rtol)
+
+
+def test_schedule_tables_known_answers():
+    g = golden("schedulers.npz")
+    v1 = osch.linear_tables(100, 0.00085, 0.012)
+    v2 = osch.linear_tables(500, 0.00005, 0.015)
+    cs = osch.cosine_tables(2000)
+    names = {"betas": "betas", "alphas": "alphas", "acp": "alpha_cum_prod",
+             "sqrt_acp": "sqrt_alpha_cum_prod", "sqrt_1m_acp": "sqrt_one_minus_alpha_cum_prod"}
+    for mine, ref in names.items():
+        assert torch.equal(v1[mine], g["v1_" + ref]), mine
+        assert torch.equal(v2[mine], g["v2_" + ref]), mine
+    assert torch.equal(cs["acp"], g["cos_alphas_cumprod"])
+    # SURVEY 8c known answers
+    close(v1["acp"][[0, 49, 99]], torch.tensor([0.99914998, 0.88042337, 0.58399236]), atol=1e-7,
+          rtol=0)
+    close(v2["acp"][[0, 249, 499]], torch.tensor([0.99994999, 0.67591095, 0.06946355]),
+          atol=1e-7, rtol=0)
+    close(cs["acp"][0], torch.tensor(0.99984455), atol=1e-7, rtol=0)
+
+
+def test_q_sample():
+    g = golden("schedulers.npz")
+    tab = osch.linear_tables(100, 0.00085, 0.012)
+    assert torch.equal(osch.q_sample(tab, g["qs_x0"], g["qs_eps"], g["qs_t"]), g["qs_xt"])
+
+
+def test_p_sample_variants():
+    g = golden("schedulers.npz")
+    xt, ep = g["ps_xt"], g["ps_eps"]
+    cases = (("v1", osch.linear_tables(100, 0.00085, 0.012), osch.p_sample_v1, (0, 1, 50, 99)),
+             ("v2", osch.linear_tables(500, 0.00005, 0.015), osch.p_sample_v2, (0, 249, 499)),
+             ("cos", osch.cosine_tables(2000), osch.p_sample_cosine, (0, 1, 1000, 1999)))
+    for tag, tab, fn, ts in cases:
+        for ti in ts:
+            prev, x0 = fn(tab, xt, ep, torch.tensor([ti]), g[f"{tag}_t{ti}_z"])
+            close(prev, g[f"{tag}_t{ti}_prev"], atol=1e-6, rtol=1e-6)
+            close(x0, g[f"{tag}_t{ti}_x0"], atol=1e-6, rtol=1e-6)
+
+
+def test_timestep_embedding():
+    g = golden("schedulers.npz")
+    for dim in (64, 65, 128):
+        assert torch.equal(onn.timestep_embedding(g["temb_t"], dim), g[f"temb_{dim}"])
+
+
+def test_group_norm_silu_fwd_bwd():
+    g = golden("blocks.npz")
+    x = seeded((2, 64, 2, 6, 6), 20).requires_grad_(True)
+    w = g["gn_w"].clone().requires_grad_(True)
+    b = g["gn_b"].clone().requires_grad_(True)
+    y = onn.group_norm(x, w, b, silu=True)
+    close(y, g["gn_y"])
+    y.backward(seeded(y.shape, 22))
+    close(x.grad, g["gn_dx"], atol=1e-5)
+    close(w.grad, g["gn_dw"], atol=1e-4)
+    close(b.grad, g["gn_db"], atol=1e-4)
+    x2 = (seeded((2, 128, 40), 23) * 3 + 1.5).requires_grad_(True)
+    y2 = onn.group_norm(x2, g["gn2_w"], g["gn2_b"])
+    close(y2, g["gn2_y"])
+
+
+def _block_params(module_shapes, seed):
+    return init_params(module_shapes, seed)
+
+
+def test_resblock3d():
+    g = golden("blocks.npz")
+    shapes = {"in_layers.0.weight": (64,), "in_layers.0.bias": (64,),
+              "in_layers.2.weight": (128, 64, 3, 3, 3), "in_layers.2.bias": (128,),
+              "emb_layers.1.weight": (128, 256), "emb_layers.1.bias": (128,),
+              "out_layers.0.weight": (128,), "out_layers.0.bias": (128,),
+              "out_layers.3.weight": (128, 128, 3, 3, 3), "out_layers.3.bias": (128,),
+              "skip_connection.weight": (128, 64, 1, 1, 1), "skip_connection.bias": (128,)}
+    P = {k: v.requires_grad_(True) for k, v in init_params(shapes, 30).items()}
+    x = seeded((2, 64, 2, 6, 6), 31).requires_grad_(True)
+    emb = seeded((2, 256), 32).requires_grad_(True)
+    y = onn.resblock(P, "", x, emb)
+    close(y, g["rb_y"], atol=1e-5, rtol=1e-4)
+    y.backward(seeded(y.shape, 33))
+    close(x.grad, g["rb_dx"], atol=1e-4, rtol=1e-4)
+    close(emb.grad, g["rb_demb"], atol=1e-4, rtol=1e-4)
+    close(P["in_layers.2.weight"].grad, g["rb_d_in_layers.2.weight"], atol=1e-4, rtol=1e-4)
+
+
+def test_attention_block_joint_and_heads():
+    g = golden("blocks.npz")
+    shapes = {"norm.weight": (64,), "norm.bias": (64,), "qkv.weight": (192, 64, 1),
+              "qkv.bias": (192,), "proj_out.weight": (64, 64, 1), "proj_out.bias": (64,)}
+    P = {k: v.requires_grad_(True) for k, v in init_params(shapes, 40).items()}
+    x = seeded((2, 64, 2, 6, 6), 41).requires_grad_(True)
+    y = onn.attention_block(P, "", x)
+    close(y, g["ab_y"], atol=1e-5, rtol=1e-4)
+    y.backward(seeded(y.shape, 42))
+    close(x.grad, g["ab_dx"], atol=1e-4, rtol=1e-4)
+    close(P["qkv.weight"].grad, g["ab_d_qkv_w"], atol=1e-4, rtol=1e-4)
+    for tag, legacy in (("abh", True), ("abn", False)):
+        P = init_params(shapes, 43)
+        x = seeded((1, 64, 10, 10), 44)
+        y = onn.attention_block(P, "", x, heads=2, legacy=legacy)
+        close(y, g[f"{tag}_y"], atol=1e-5, rtol=1e-4)
+
+
+def test_spatial_temporal_regrouping():
+    g = golden("blocks.npz")
+    B, C, T, HW = 2, 64, 3, 36
+    qkv = seeded((B, 3 * C, T * HW), 46)
+    for mode, key in (("spatial", "st_spatial"), ("temporal", "st_temporal"),
+                      ("joint", "st_joint")):
+        out = onn.qkv_attention(qkv, 1, mode=mode, spatial=(T, 6, 6))
+        close(out, g[key], atol=1e-5, rtol=1e-5)
+
+
+def test_up_down_sample():
+    g = golden("blocks.npz")
+    P = init_params({"conv.weight": (64, 64, 3, 3, 3), "conv.bias": (64,)}, 50)
+    close(onn.upsample_block(P, "", seeded((1, 64, 2, 5, 5), 51), 3), g["up_y"], atol=1e-5)
+    P = init_params({"op.weight": (64, 64, 3, 3, 3), "op.bias": (64,)}, 53)
+    close(onn.downsample_block(P, "", seeded((1, 64, 2, 9, 9), 54), 3), g["dn_y"], atol=1e-5)
+
+
+def test_plan_matches_reference_state_dict_counts():
+    # 306 UNet keys at the train.py config
+    shapes = param_shapes(build_plan(**FULL2D))
+    assert len(shapes) == 306
+    assert shapes["input_blocks.1.1.qkv.weight"] == (192, 64, 1)
+    n3 = sum(torch.Size(s).numel() for s in param_shapes(build_plan(**dict(FULL2D, dims=3))).values())
+    assert n3 == 42062595  # 3-D core
+    n2 = sum(torch.Size(s).numel() for s in shapes.values())
+    assert n2 == 16250883
+
+
+def test_tiny3d_unet_forward_and_grads():
+    g = golden("unet_tiny3d.npz")
+    plan = build_plan(**TINY3D)
+    P = {k: v.requires_grad_(True) for k, v in init_params(param_shapes(plan), 1234).items()}
+    x = seeded(TINY3D_SHAPE, 60, "uniform")
+    y = unet_forward(P, plan, x, g["t"])
+    assert rel_l2(y, g["y"]) < 1e-5
+    loss = F.mse_loss(y, seeded((1, 3) + TINY3D_SHAPE[2:], 61))
+    close(loss, g["loss"], atol=1e-6, rtol=1e-5)
+    loss.backward()
+    for k in ("input_blocks.0.0.weight", "out.2.weight", "input_blocks.3.1.qkv.weight"):
+        assert rel_l2(P[k].grad, g["grad_" + k]) < 1e-4, k
+
+
+def test_full2d_unet_and_audio_conditioning():
+    g = golden("unet_full2d.npz")
+    plan = build_plan(**FULL2D)
+    P = init_params(param_shapes(plan), 1234)
+    y = unet_forward(P, plan, seeded(FULL2D_SHAPE, 62, "uniform"), g["t"])
+    assert rel_l2(y, g["y"]) < 1e-5
+    ga = golden("unet_audio2d.npz")
+    A = init_params(audio_param_shapes(768, 128), 77)
+    P.update(A)
+    feats = audio_conditioned_input(P, seeded((2, 3, 32, 32), 64, "uniform"),
+                                    seeded((2, 3, 16, 16), 65, "uniform"), seeded((2, 768), 66),
+                                    128)
+    y = unet_forward(P, plan, feats, ga["t"])
+    assert rel_l2(y, ga["y"]) < 1e-5
