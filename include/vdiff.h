@@ -107,17 +107,43 @@ int vd_ddim_step(const void* xt, const void* eps, const void* z, void* x_prev,
  * S = T*H*W; gamma/beta fp32[C]; mean/rstd fp32[B*G] (saved for backward).
  * (The ResBlock emb-add that precedes out_layers' GN is fused into the
  * producing conv's epilogue via vd_conv3d_fwd's chan_add.) */
+/* drop_p > 0 also fuses the train-mode nn.Dropout that follows the SiLU in
+ * ResBlock.out_layers (unet.py:218-225): element i is kept with probability
+ * 1 - drop_p (scaled by 1/(1-drop_p)) by a counter-based hash of (seed, i);
+ * the backward regenerates the same mask from the same seed. */
 size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G);
 int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta,
                           void* y, float* mean, float* rstd, int B, int64_t S,
-                          int C, int G, float eps, int silu, int dtype,
-                          void* workspace, void* stream);
-/* dx = d/dx of silu(GN(x)); dgamma/dbeta are fp32[C] and OVERWRITTEN. */
+                          int C, int G, float eps, int silu, float drop_p,
+                          uint64_t seed, int dtype, void* workspace,
+                          void* stream);
+/* dx = d/dx of dropout(silu(GN(x))); dgamma/dbeta are fp32[C], OVERWRITTEN. */
 int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma,
                           const float* beta, const float* mean,
                           const float* rstd, void* dx, float* dgamma,
                           float* dbeta, int B, int64_t S, int C, int G,
-                          int silu, int dtype, void* workspace, void* stream);
+                          int silu, float drop_p, uint64_t seed, int dtype,
+                          void* workspace, void* stream);
+
+/* ---- SiLU on flat tensors (time-embedding MLP, ResBlock.emb_layers:
+ * unet.py:483-487, 211-217).  bwd: dx = dy * silu'(x). */
+int vd_silu(const void* x, void* y, int64_t n, int dtype, void* stream);
+int vd_silu_bwd(const void* x, const void* dy, void* dx, int64_t n, int dtype,
+                void* stream);
+
+/* ---- UNetAudio conditioning concat (unet_audio.py:52-61) -------------
+ * out[b][t][y][x][:] = [ image[b][t][y][x][0:Cx] | imc[b][ys][xs][0:Ci] |
+ *                        audio[b][t][0:Ca] | zeros up to out_cstride ]
+ * with (ys, xs) the torch "nearest" source of (y, x) for an (h, w) -> (H, W)
+ * resize (the 1x1 cond conv commutes with it and runs at (h, w)).  imc is
+ * broadcast over T (one reference image per clip) and audio over (H, W).
+ * bwd: d_imc[b][h][w][Ci] and d_audio[b][T][Ca] (fp32) are OVERWRITTEN. */
+int vd_cond_concat(const void* image, const void* imc, const void* audio,
+                   void* out, int B, int T, int H, int W, int Cx, int h, int w,
+                   int Ci, int Ca, int out_cstride, int dtype, void* stream);
+int vd_cond_concat_bwd(const void* dout, float* d_imc, float* d_audio, int B,
+                       int T, int H, int W, int Cx, int h, int w, int Ci,
+                       int Ca, int out_cstride, int dtype, void* stream);
 
 /* ---- Upsample (nearest, x2 on H and W) --------------------------------
  * replaces unet.py:112-122 F.interpolate(..., mode="nearest") with the

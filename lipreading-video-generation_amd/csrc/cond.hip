@@ -1,0 +1,172 @@
+// cond.hip -- UNetAudio conditioning assembly and flat SiLU.
+//
+// vd_cond_concat replaces the broadcast + nearest-resize + th.cat of
+// UNetAudio.forward (reference unet_audio.py:52-61): it writes the
+// [image | image-cond | audio | zero pad] channels of every pixel straight
+// into the channels-last input buffer of the first conv, so the
+// expand()-ed audio/image tensors are never materialised.
+// vd_silu / vd_silu_bwd serve the timestep-embedding MLP (unet.py:483-487)
+// and ResBlock.emb_layers (unet.py:211-217).
+#include "vd_common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t work) {
+  int64_t g = vd_cdiv(work, kBlock);
+  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+
+// torch "nearest" source index for an in -> out resize
+__device__ __forceinline__ int nearest_src(int dst, int in, int out) {
+  const float scale = (float)in / (float)out;
+  int s = (int)floorf((float)dst * scale);
+  return s < in - 1 ? s : in - 1;
+}
+
+template <typename T>
+__global__ void silu_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    Elem<T>::st(y + i, silu_f(Elem<T>::ld(x + i)));
+}
+
+template <typename T>
+__global__ void silu_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                T* __restrict__ dx, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float z = Elem<T>::ld(x + i);
+    const float s = 1.f / (1.f + __expf(-z));
+    Elem<T>::st(dx + i, Elem<T>::ld(dy + i) * s * (1.f + z * (1.f - s)));
+  }
+}
+
+// one thread per (pixel, output channel)
+template <typename T>
+__global__ void cond_concat_kernel(const T* __restrict__ image, const T* __restrict__ imc,
+                                   const T* __restrict__ audio, T* __restrict__ out, int B, int T_,
+                                   int H, int W, int Cx, int h, int w, int Ci, int Ca, int Cs) {
+  const int64_t n = (int64_t)B * T_ * H * W * Cs;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cs);
+    int64_t p = i / Cs;
+    const int x = (int)(p % W);
+    p /= W;
+    const int y = (int)(p % H);
+    p /= H;
+    const int t = (int)(p % T_);
+    const int b = (int)(p / T_);
+    float v = 0.f;
+    if (c < Cx) {
+      v = Elem<T>::ld(image + ((((int64_t)b * T_ + t) * H + y) * W + x) * Cx + c);
+    } else if (c < Cx + Ci) {
+      const int ys = nearest_src(y, h, H), xs = nearest_src(x, w, W);
+      v = Elem<T>::ld(imc + (((int64_t)b * h + ys) * w + xs) * Ci + (c - Cx));
+    } else if (c < Cx + Ci + Ca) {
+      v = Elem<T>::ld(audio + ((int64_t)b * T_ + t) * Ca + (c - Cx - Ci));
+    }
+    Elem<T>::st(out + i, v);
+  }
+}
+
+// d_audio[b][t][c] = sum over (y, x); grid (B*T, chunks of rows), atomics across chunks
+template <typename T>
+__global__ void cond_audio_bwd_kernel(const T* __restrict__ dout, float* __restrict__ da, int H,
+                                      int W, int off, int Ca, int Cs, int rows_per_block) {
+  const int bt = blockIdx.x;
+  const int64_t HW = (int64_t)H * W;
+  const int64_t p0 = (int64_t)blockIdx.y * rows_per_block;
+  int64_t p1 = p0 + rows_per_block;
+  if (p1 > HW) p1 = HW;
+  for (int c = threadIdx.x; c < Ca; c += blockDim.x) {
+    float s = 0.f;
+    for (int64_t p = p0; p < p1; ++p)
+      s += Elem<T>::ld(dout + ((int64_t)bt * HW + p) * Cs + off + c);
+    atomicAdd(da + (int64_t)bt * Ca + c, s);
+  }
+}
+
+// d_imc[b][ys][xs][c] += sum over t and the (y, x) whose nearest source is (ys, xs)
+template <typename T>
+__global__ void cond_imc_bwd_kernel(const T* __restrict__ dout, float* __restrict__ di, int B,
+                                    int T_, int H, int W, int off, int h, int w, int Ci, int Cs) {
+  const int64_t n = (int64_t)B * H * W * Ci;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Ci);
+    int64_t p = i / Ci;
+    const int x = (int)(p % W);
+    p /= W;
+    const int y = (int)(p % H);
+    const int b = (int)(p / H);
+    float s = 0.f;
+    for (int t = 0; t < T_; ++t)
+      s += Elem<T>::ld(dout + ((((int64_t)b * T_ + t) * H + y) * W + x) * Cs + off + c);
+    const int ys = nearest_src(y, h, H), xs = nearest_src(x, w, W);
+    atomicAdd(di + (((int64_t)b * h + ys) * w + xs) * Ci + c, s);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int vd_silu(const void* x, void* y, int64_t n, int dtype, void* stream) {
+  VD_REQUIRE(x && y && n > 0, "bad silu arguments");
+  return VD_DISPATCH_DTYPE(dtype, T, {
+    silu_kernel<T><<<grid_for(n), kBlock, 0, VD_STREAM(stream)>>>((const T*)x, (T*)y, n);
+  });
+}
+
+int vd_silu_bwd(const void* x, const void* dy, void* dx, int64_t n, int dtype, void* stream) {
+  VD_REQUIRE(x && dy && dx && n > 0, "bad silu_bwd arguments");
+  return VD_DISPATCH_DTYPE(dtype, T, {
+    silu_bwd_kernel<T><<<grid_for(n), kBlock, 0, VD_STREAM(stream)>>>((const T*)x, (const T*)dy,
+                                                                      (T*)dx, n);
+  });
+}
+
+int vd_cond_concat(const void* image, const void* imc, const void* audio, void* out, int B, int T,
+                   int H, int W, int Cx, int h, int w, int Ci, int Ca, int out_cstride, int dtype,
+                   void* stream) {
+  VD_REQUIRE(image && out, "null tensor");
+  VD_REQUIRE((Ci == 0 || imc) && (Ca == 0 || audio), "null conditioning tensor");
+  VD_REQUIRE(B > 0 && T > 0 && H > 0 && W > 0 && Cx > 0 && h > 0 && w > 0, "bad shape");
+  VD_REQUIRE(out_cstride >= Cx + Ci + Ca, "out_cstride %d < %d", out_cstride, Cx + Ci + Ca);
+  const int64_t n = (int64_t)B * T * H * W * out_cstride;
+  return VD_DISPATCH_DTYPE(dtype, Tp, {
+    cond_concat_kernel<Tp><<<grid_for(n), kBlock, 0, VD_STREAM(stream)>>>(
+        (const Tp*)image, (const Tp*)imc, (const Tp*)audio, (Tp*)out, B, T, H, W, Cx, h, w, Ci,
+        Ca, out_cstride);
+  });
+}
+
+int vd_cond_concat_bwd(const void* dout, float* d_imc, float* d_audio, int B, int T, int H, int W,
+                       int Cx, int h, int w, int Ci, int Ca, int out_cstride, int dtype,
+                       void* stream) {
+  VD_REQUIRE(dout, "null tensor");
+  VD_REQUIRE(B > 0 && T > 0 && H > 0 && W > 0 && h > 0 && w > 0, "bad shape");
+  hipStream_t st = VD_STREAM(stream);
+  if (d_imc && Ci > 0 && hipMemsetAsync(d_imc, 0, sizeof(float) * B * h * w * Ci, st))
+    return vd::fail(VD_ELAUNCH, "memset d_imc");
+  if (d_audio && Ca > 0 && hipMemsetAsync(d_audio, 0, sizeof(float) * B * T * Ca, st))
+    return vd::fail(VD_ELAUNCH, "memset d_audio");
+  return VD_DISPATCH_DTYPE(dtype, Tp, {
+    if (d_audio && Ca > 0) {
+      const int rows = 256;
+      dim3 grid((unsigned)(B * T), (unsigned)vd_cdiv((int64_t)H * W, rows));
+      cond_audio_bwd_kernel<Tp><<<grid, 128, 0, st>>>((const Tp*)dout, d_audio, H, W, Cx + Ci, Ca,
+                                                      out_cstride, rows);
+    }
+    if (d_imc && Ci > 0) {
+      const int64_t n = (int64_t)B * H * W * Ci;
+      cond_imc_bwd_kernel<Tp><<<grid_for(n), kBlock, 0, st>>>((const Tp*)dout, d_imc, B, T, H, W,
+                                                              Cx, h, w, Ci, out_cstride);
+    }
+  });
+}
+
+}  // extern "C"

@@ -51,6 +51,15 @@ __device__ __forceinline__ Stat chan(Stat a, Stat b) {
   return r;
 }
 
+// train-mode dropout after the SiLU (ResBlock.out_layers, unet.py:221)
+struct Drop {
+  float p, inv_keep;
+  uint64_t seed;
+  __device__ __forceinline__ float mul(int64_t idx) const {
+    return p > 0.f ? dropout_mul(seed, idx, p, inv_keep) : 1.f;
+  }
+};
+
 // ---------------------------------------------------------------- forward
 // grid (nchunk, B).  Per WG: per-group (n, mean, M2) over its chunk.
 template <typename T>
@@ -148,7 +157,7 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict_
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
                                                             T* __restrict__ y, int B, int64_t S,
-                                                            int C, int G) {
+                                                            int C, int G, Drop drop) {
   const int nvec = C / kVec;
   const int cpg = C / G;
   const int64_t n = (int64_t)B * S * nvec;
@@ -164,7 +173,7 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict_
       const int g = b * G + c / cpg;
       const float sc = gamma[c] * rstd[g];
       const float z = (v[j] - mean[g]) * sc + beta[c];
-      v[j] = SILU ? silu_f(z) : z;
+      v[j] = (SILU ? silu_f(z) : z) * drop.mul(i * kVec + j);
     }
     store8(y + i * kVec, v);
   }
@@ -176,7 +185,8 @@ template <typename T, bool SILU>
 __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
-    int64_t S, int C, int G, int64_t chunk_px, int rows_per_iter, float* __restrict__ part) {
+    int64_t S, int C, int G, int64_t chunk_px, int rows_per_iter, float* __restrict__ part,
+    Drop drop) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh = reinterpret_cast<float2*>(smem);  // [rows_per_iter][C]
   const int nvec = C / kVec;
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
 #pragma unroll
       for (int j = 0; j < kVec; ++j) {
         const float xh = (v[j] - mu[j]) * rs[j];
-        float dz = d[j];
+        float dz = d[j] * drop.mul(((int64_t)b * S + p) * C + cv * kVec + j);
         if (SILU) {
           const float z = xh * ga[j] + be[j];
           const float sg = 1.f / (1.f + __expf(-z));
@@ -281,7 +291,8 @@ template <typename T, bool SILU>
 __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
-    const float* __restrict__ coef, T* __restrict__ dx, int B, int64_t S, int C, int G) {
+    const float* __restrict__ coef, T* __restrict__ dx, int B, int64_t S, int C, int G,
+    Drop drop) {
   const int nvec = C / kVec;
   const int cpg = C / G;
   const int64_t n = (int64_t)B * S * nvec;
@@ -298,7 +309,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
       const int g = b * G + c / cpg;
       const float rs = rstd[g];
       const float xh = (v[j] - mean[g]) * rs;
-      float dz = d[j];
+      float dz = d[j] * drop.mul(i * kVec + j);
       if (SILU) {
         const float z = xh * gamma[c] + beta[c];
         const float sg = 1.f / (1.f + __expf(-z));
@@ -341,10 +352,14 @@ size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G) {
 
 int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, void* y,
                           float* mean, float* rstd, int B, int64_t S, int C, int G, float eps,
-                          int silu, int dtype, void* workspace, void* stream) {
+                          int silu, float drop_p, uint64_t seed, int dtype, void* workspace,
+                          void* stream) {
   int rc = gn_check(x, B, S, C, G);
   if (rc) return rc;
   VD_REQUIRE(gamma && beta && y && mean && rstd && workspace, "null argument");
+  VD_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "dropout p=%f out of [0, 1)", drop_p);
+  VD_REQUIRE(drop_p == 0.f || silu, "dropout is fused only after SiLU");
+  const Drop drop{drop_p, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, seed};
   GNPlan p = gn_plan(B, S, C);
   float* part = reinterpret_cast<float*>(workspace);
   hipStream_t st = VD_STREAM(stream);
@@ -356,21 +371,23 @@ int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, 
     const int grid = apply_grid((int64_t)B * S * (C / kVec));
     if (silu)
       gn_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
-                                                          (T*)y, B, S, C, G);
+                                                          (T*)y, B, S, C, G, drop);
     else
       gn_apply_kernel<T, false><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
-                                                           (T*)y, B, S, C, G);
+                                                           (T*)y, B, S, C, G, drop);
   });
 }
 
 int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, const float* beta,
                           const float* mean, const float* rstd, void* dx, float* dgamma,
-                          float* dbeta, int B, int64_t S, int C, int G, int silu, int dtype,
-                          void* workspace, void* stream) {
+                          float* dbeta, int B, int64_t S, int C, int G, int silu, float drop_p,
+                          uint64_t seed, int dtype, void* workspace, void* stream) {
   int rc = gn_check(x, B, S, C, G);
   if (rc) return rc;
   VD_REQUIRE(dy && gamma && beta && mean && rstd && dx && dgamma && dbeta && workspace,
              "null argument");
+  VD_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "dropout p=%f out of [0, 1)", drop_p);
+  const Drop drop{drop_p, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, seed};
   GNPlan p = gn_plan(B, S, C);
   float* part = reinterpret_cast<float*>(workspace);
   float* coef = part + (size_t)B * p.nchunk * C * 2;
@@ -381,22 +398,22 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
     if (silu)
       gn_bwd_reduce_kernel<T, true><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part);
+          p.rows_per_iter, part, drop);
     else
       gn_bwd_reduce_kernel<T, false><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part);
+          p.rows_per_iter, part, drop);
     gn_bwd_finalize_kernel<<<1, kThreads, 2 * C * sizeof(float), st>>>(part, B, p.nchunk, C, G,
                                                                        S, gamma, coef, dgamma,
                                                                        dbeta);
     if (silu)
       gn_bwd_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, (const T*)dy, gamma,
                                                               beta, mean, rstd, coef, (T*)dx, B,
-                                                              S, C, G);
+                                                              S, C, G, drop);
     else
       gn_bwd_apply_kernel<T, false><<<grid, kThreads, 0, st>>>((const T*)x, (const T*)dy, gamma,
                                                                beta, mean, rstd, coef, (T*)dx,
-                                                               B, S, C, G);
+                                                               B, S, C, G, drop);
   });
 }
 

@@ -79,6 +79,16 @@ __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// counter-based dropout keep mask (splitmix64 of seed + idx); returns 0 or 1/(1-p)
+__device__ __forceinline__ float dropout_mul(uint64_t seed, int64_t idx, float p, float inv_keep) {
+  uint64_t z = seed + (uint64_t)idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+  return u >= p ? inv_keep : 0.f;
+}
+
 __device__ __forceinline__ float silu_f(float z) { return z / (1.0f + __expf(-z)); }
 
 __device__ __forceinline__ float wave_sum(float v) {

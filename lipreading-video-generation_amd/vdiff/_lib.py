@@ -19,6 +19,7 @@ ABI_VERSION = 1
 _vp = C.c_void_p
 _i = C.c_int
 _i64 = C.c_int64
+_u64 = C.c_uint64
 _f = C.c_float
 _sz = C.c_size_t
 
@@ -49,10 +50,14 @@ _SIGS = {
     "vd_p_sample_cosine": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i, _vp]),
     "vd_ddim_step": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _i64, _i64, _i, _vp]),
     "vd_groupnorm_workspace_size": (_sz, [_i, _i64, _i, _i]),
-    "vd_groupnorm_silu_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i64, _i, _i, _f, _i, _i, _vp,
-                                   _vp]),
+    "vd_groupnorm_silu_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i64, _i, _i, _f, _i, _f,
+                                   _u64, _i, _vp, _vp]),
     "vd_groupnorm_silu_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i64, _i, _i,
-                                   _i, _i, _vp, _vp]),
+                                   _i, _f, _u64, _i, _vp, _vp]),
+    "vd_silu": (_i, [_vp, _vp, _i64, _i, _vp]),
+    "vd_silu_bwd": (_i, [_vp, _vp, _vp, _i64, _i, _vp]),
+    "vd_cond_concat": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "vd_cond_concat_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "vd_upsample_nearest_hw": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),
     "vd_upsample_nearest_hw_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),
     "vd_conv3d_fwd": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

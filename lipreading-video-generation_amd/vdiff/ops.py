@@ -169,7 +169,8 @@ def ddim_step(xt, eps, t, t_prev, acp, eta=0.0, z=None, clip=False):
 # --------------------------------------------------------------- GroupNorm+SiLU
 class GroupNormSiLUFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool):
+    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float,
+                seed: int):
         _gpu(x, gamma, beta)
         x = to_cl(x)
         B, Cc, S = x.shape[0], x.shape[1], _spatial(x)
@@ -182,15 +183,16 @@ class GroupNormSiLUFn(torch.autograd.Function):
         ws = torch.empty(_lib.lib().vd_groupnorm_workspace_size(B, S, Cc, groups),
                          dtype=torch.uint8, device=x.device)
         _lib.call("vd_groupnorm_silu_fwd", _p(x), _p(g32), _p(b32), _p(y), _p(mean), _p(rstd), B,
-                  S, Cc, groups, float(eps), int(silu), dt, _p(ws), _stream(x))
+                  S, Cc, groups, float(eps), int(silu), float(drop_p), int(seed), dt, _p(ws),
+                  _stream(x))
         ctx.save_for_backward(x, g32, b32, mean, rstd)
-        ctx.cfg = (groups, silu, gamma.dtype)
+        ctx.cfg = (groups, silu, gamma.dtype, float(drop_p), int(seed))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, g32, b32, mean, rstd = ctx.saved_tensors
-        groups, silu, pdt = ctx.cfg
+        groups, silu, pdt, drop_p, seed = ctx.cfg
         dy = to_cl(dy).to(x.dtype)
         B, Cc, S = x.shape[0], x.shape[1], _spatial(x)
         dx = torch.empty_like(x)
@@ -199,13 +201,96 @@ class GroupNormSiLUFn(torch.autograd.Function):
         ws = torch.empty(_lib.lib().vd_groupnorm_workspace_size(B, S, Cc, groups),
                          dtype=torch.uint8, device=x.device)
         _lib.call("vd_groupnorm_silu_bwd", _p(x), _p(dy), _p(g32), _p(b32), _p(mean), _p(rstd),
-                  _p(dx), _p(dg), _p(db), B, S, Cc, groups, int(silu), _dtype(x), _p(ws),
-                  _stream(x))
-        return dx, dg.to(pdt), db.to(pdt), None, None, None
+                  _p(dx), _p(dg), _p(db), B, S, Cc, groups, int(silu), drop_p, seed, _dtype(x),
+                  _p(ws), _stream(x))
+        return dx, dg.to(pdt), db.to(pdt), None, None, None, None, None
 
 
-def group_norm_silu(x, weight, bias, groups=32, eps=1e-5, silu=True):
-    return GroupNormSiLUFn.apply(x, weight, bias, groups, eps, silu)
+def new_seed() -> int:
+    """Host-side 63-bit seed from torch's CPU generator (no device sync)."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def group_norm_silu(x, weight, bias, groups=32, eps=1e-5, silu=True, dropout=0.0, seed=None):
+    """silu(GroupNorm(x)) [then train-mode dropout], fp32 statistics."""
+    if dropout > 0.0 and seed is None:
+        seed = new_seed()
+    return GroupNormSiLUFn.apply(x, weight, bias, groups, eps, silu, float(dropout),
+                                 int(seed or 0))
+
+
+class SiLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _gpu(x)
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _lib.call("vd_silu", _p(x), _p(y), x.numel(), _dtype(x), _stream(x))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous().to(x.dtype)
+        dx = torch.empty_like(x)
+        _lib.call("vd_silu_bwd", _p(x), _p(dy), _p(dx), x.numel(), _dtype(x), _stream(x))
+        return dx
+
+
+def silu(x):
+    return SiLUFn.apply(x)
+
+
+def linear(x, weight, bias=None):
+    """x [..., Cin] @ weight[Cout, Cin]^T + bias on the implicit-GEMM kernel (1x1 conv)."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1], 1).contiguous()
+    x2 = x2.movedim(1, -1).contiguous().movedim(-1, 1) if not is_cl(x2) else x2
+    y = conv(x2, weight.reshape(weight.shape[0], weight.shape[1], 1), bias)
+    return y.reshape(*lead, weight.shape[0])
+
+
+class CondConcatFn(torch.autograd.Function):
+    """[image | nearest-resized image-cond | audio | zero pad] -> channels-last buffer."""
+
+    @staticmethod
+    def forward(ctx, image, imc, audio, cpad: int):
+        _gpu(image, imc, audio)
+        idt0, adt0 = imc.dtype, audio.dtype
+        image = to_cl(image)
+        dt = image.dtype
+        five = image.dim() == 5
+        B, Cx = image.shape[:2]
+        T = image.shape[2] if five else 1
+        H, W = image.shape[-2:]
+        imc = to_cl(imc.to(dt))  # [B, Ci, h, w]
+        Ci, h, w = imc.shape[1], imc.shape[2], imc.shape[3]
+        audio = audio.to(dt).contiguous()  # [B, T, Ca]
+        Ca = audio.shape[-1]
+        Ct = Cx + Ci + Ca
+        cs = max(cpad, Ct)
+        shape = [B, cs, T, H, W] if five else [B, cs, H, W]
+        out = empty_cl(shape, dt, image.device)
+        _lib.call("vd_cond_concat", _p(image), _p(imc), _p(audio), _p(out), B, T, H, W, Cx, h, w,
+                  Ci, Ca, cs, _DT[dt], _stream(image))
+        ctx.geom = (B, T, H, W, Cx, h, w, Ci, Ca, cs, idt0, adt0)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, T, H, W, Cx, h, w, Ci, Ca, cs, idt, adt = ctx.geom
+        dout = to_cl(dout)
+        d_imc = torch.empty(B, h, w, Ci, dtype=torch.float32, device=dout.device)
+        d_aud = torch.empty(B, T, Ca, dtype=torch.float32, device=dout.device)
+        _lib.call("vd_cond_concat_bwd", _p(dout), _p(d_imc), _p(d_aud), B, T, H, W, Cx, h, w, Ci,
+                  Ca, cs, _dtype(dout), _stream(dout))
+        d_img = dout[:, :Cx]
+        return d_img, d_imc.permute(0, 3, 1, 2).to(idt), d_aud.to(adt), None
+
+
+def cond_concat(image, imc, audio, cpad=0):
+    return CondConcatFn.apply(image, imc, audio, cpad)
 
 
 # --------------------------------------------------------------- Upsample

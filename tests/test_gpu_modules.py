@@ -1,0 +1,288 @@
+"""Drop-in modules (vdiff.nn / vdiff.unet_audio) vs the reference golden vectors and the
+oracle: fp32 parity mode (north-star bar: rel-L2 <= 1e-3; observed ~1e-6) and bf16
+throughput mode (rel-L2 <= 3e-2 vs fp32 reference)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import nn as onn
+from oracle.fixtures import FULL2D, FULL2D_SHAPE, TINY3D, TINY3D_SHAPE, rel_l2, seeded
+from oracle.unet import audio_param_shapes, build_plan, init_params, param_shapes, unet_forward
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _load(module, seed):
+    shapes = {k: tuple(v.shape) for k, v in module.state_dict().items()}
+    P = init_params(shapes, seed)
+    module.load_state_dict(P)
+    return P
+
+
+def test_state_dict_keys_match_reference_plan():
+    from vdiff.nn import UNetModel
+    m = UNetModel(image_size=32, **FULL2D)
+    ref = param_shapes(build_plan(**FULL2D))
+    sd = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert list(sd) == list(ref)
+    assert sd == dict(ref)
+
+
+def test_resblock3d_golden():
+    from vdiff.nn import ResBlock
+    g = golden("blocks.npz")
+    rb = ResBlock(64, 256, 0.0, out_channels=128, dims=3)
+    _load(rb, 30)
+    rb = rb.to(dev)
+    x = seeded((2, 64, 2, 6, 6), 31).to(dev).requires_grad_(True)
+    emb = seeded((2, 256), 32).to(dev).requires_grad_(True)
+    y = rb(x, emb)
+    assert rel_l2(y, g["rb_y"]) < 1e-5
+    y.backward(seeded(y.shape, 33).to(dev))
+    assert rel_l2(x.grad, g["rb_dx"]) < 1e-5
+    assert rel_l2(emb.grad, g["rb_demb"]) < 1e-5
+    named = dict(rb.named_parameters())
+    for k in ("in_layers.2.weight", "skip_connection.weight", "out_layers.0.weight",
+              "emb_layers.1.weight", "out_layers.3.bias"):
+        assert rel_l2(named[k].grad, g["rb_d_" + k]) < 1e-5, k
+
+
+def test_resblock2d_identity_skip_golden():
+    from vdiff.nn import ResBlock
+    g = golden("blocks.npz")
+    rb = ResBlock(64, 256, 0.0, dims=2)
+    _load(rb, 34)
+    rb = rb.to(dev)
+    x = seeded((2, 64, 10, 10), 35).to(dev).requires_grad_(True)
+    y = rb(x, seeded((2, 256), 36).to(dev))
+    assert rel_l2(y, g["rb2_y"]) < 1e-5
+    y.backward(seeded(y.shape, 37).to(dev))
+    assert rel_l2(x.grad, g["rb2_dx"]) < 1e-5
+    assert rel_l2(rb.in_layers[2].weight.grad, g["rb2_d_in_w"]) < 1e-5
+
+
+def test_attention_block_golden():
+    from vdiff.nn import AttentionBlock
+    g = golden("blocks.npz")
+    ab = AttentionBlock(64, num_heads=1)
+    _load(ab, 40)
+    ab = ab.to(dev)
+    x = seeded((2, 64, 2, 6, 6), 41).to(dev).requires_grad_(True)
+    y = ab(x)
+    assert rel_l2(y, g["ab_y"]) < 1e-5
+    y.backward(seeded(y.shape, 42).to(dev))
+    assert rel_l2(x.grad, g["ab_dx"]) < 1e-5
+    assert rel_l2(ab.qkv.weight.grad, g["ab_d_qkv_w"]) < 1e-5
+    assert rel_l2(ab.proj_out.weight.grad, g["ab_d_proj_w"]) < 1e-5
+    assert rel_l2(ab.norm.weight.grad, g["ab_d_norm_w"]) < 1e-5
+    for tag, new_order in (("abh", False), ("abn", True)):
+        m = AttentionBlock(64, num_heads=2, use_new_attention_order=new_order)
+        _load(m, 43)
+        m = m.to(dev)
+        x = seeded((1, 64, 10, 10), 44).to(dev).requires_grad_(True)
+        y = m(x)
+        assert rel_l2(y, g[f"{tag}_y"]) < 1e-5, tag
+        y.backward(seeded(y.shape, 45).to(dev))
+        assert rel_l2(x.grad, g[f"{tag}_dx"]) < 1e-5, tag
+        assert rel_l2(m.qkv.weight.grad, g[f"{tag}_d_qkv_w"]) < 1e-5, tag
+
+
+def test_up_down_golden():
+    from vdiff.nn import Downsample, Upsample
+    g = golden("blocks.npz")
+    up = Upsample(64, True, dims=3)
+    _load(up, 50)
+    up = up.to(dev)
+    x = seeded((1, 64, 2, 5, 5), 51).to(dev).requires_grad_(True)
+    y = up(x)
+    assert rel_l2(y, g["up_y"]) < 1e-5
+    y.backward(seeded(y.shape, 52).to(dev))
+    assert rel_l2(x.grad, g["up_dx"]) < 1e-5
+    assert rel_l2(up.conv.weight.grad, g["up_dw"]) < 1e-5
+    dn = Downsample(64, True, dims=3)
+    _load(dn, 53)
+    dn = dn.to(dev)
+    x = seeded((1, 64, 2, 9, 9), 54).to(dev).requires_grad_(True)
+    y = dn(x)
+    assert rel_l2(y, g["dn_y"]) < 1e-5
+    y.backward(seeded(y.shape, 55).to(dev))
+    assert rel_l2(x.grad, g["dn_dx"]) < 1e-5
+    assert rel_l2(dn.op.weight.grad, g["dn_dw"]) < 1e-5
+
+
+def _tiny3d(dtype_bf16=False, mode="joint"):
+    from vdiff.nn import UNetModel
+    m = UNetModel(image_size=64, **TINY3D, attention_mode=mode, use_bf16=dtype_bf16)
+    _load(m, 1234)
+    return m.to(dev).eval()
+
+
+def test_tiny3d_unet_golden_fp32():
+    g = golden("unet_tiny3d.npz")
+    m = _tiny3d()
+    x = seeded(TINY3D_SHAPE, 60, "uniform").to(dev)
+    y = m(x, g["t"].to(dev))
+    e = rel_l2(y, g["y"])
+    assert e < 1e-4, e  # north-star bar is 1e-3
+    loss = F.mse_loss(y, seeded((1, 3) + TINY3D_SHAPE[2:], 61).to(dev))
+    assert abs(loss.item() - g["loss"].item()) / g["loss"].item() < 1e-5
+    loss.backward()
+    named = dict(m.named_parameters())
+    for k in ("input_blocks.0.0.weight", "out.2.weight", "input_blocks.3.1.qkv.weight",
+              "middle_block.0.in_layers.0.weight", "output_blocks.0.0.skip_connection.weight",
+              "time_embed.0.weight"):
+        assert rel_l2(named[k].grad, g["grad_" + k]) < 1e-4, k
+
+
+def test_tiny3d_unet_bf16_tolerance():
+    g = golden("unet_tiny3d.npz")
+    m = _tiny3d(dtype_bf16=True)
+    y = m(seeded(TINY3D_SHAPE, 60, "uniform").to(dev), g["t"].to(dev))
+    assert y.dtype == torch.float32
+    e = rel_l2(y, g["y"])
+    assert e < 3e-2, e
+
+
+def test_full2d_unet_golden_fp32():
+    from vdiff.nn import UNetModel
+    g = golden("unet_full2d.npz")
+    m = UNetModel(image_size=32, **FULL2D)
+    _load(m, 1234)
+    m = m.to(dev).eval()
+    y = m(seeded(FULL2D_SHAPE, 62, "uniform").to(dev), g["t"].to(dev))
+    assert rel_l2(y, g["y"]) < 1e-4
+    y.backward(seeded(y.shape, 63).to(dev))
+    assert rel_l2(m.input_blocks[0][0].weight.grad, g["grad_in"]) < 1e-4
+    assert rel_l2(m.input_blocks[1][1].qkv.weight.grad, g["grad_attn"]) < 1e-4
+    assert rel_l2(m.out[2].weight.grad, g["grad_out"]) < 1e-4
+
+
+def test_unet_audio_conditioning_golden():
+    from vdiff.unet_audio import UNetAudio
+    ga = golden("unet_audio2d.npz")
+    m = UNetAudio(image_size=32, in_channels=3, model_channels=64, out_channels=3,
+                  num_res_blocks=2, attention_resolutions=(1, 2, 4), audio_feature_dim=768,
+                  projected_audio_dim=128, audio_encoder=False)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    P = init_params({k: v for k, v in shapes.items() if not k.startswith(("audio_", "cond_"))},
+                    1234)
+    P.update(init_params(audio_param_shapes(768, 128), 77))
+    m.load_state_dict(P)
+    m = m.to(dev).eval()
+    y = m(seeded((2, 3, 32, 32), 64, "uniform").to(dev),
+          seeded((2, 3, 16, 16), 65, "uniform").to(dev), seeded((2, 768), 66).to(dev),
+          ga["t"].to(dev))
+    assert rel_l2(y, ga["y"]) < 1e-4
+
+
+def test_unet_audio_5d_matches_oracle_and_trains():
+    """Frame-stack conditioning (build extension D2) vs the oracle restatement, incl. grads
+    through the concat kernel into cond_conv_in / audio_transformer."""
+    from vdiff.unet_audio import UNetAudio
+    cfg = dict(image_size=16, in_channels=3, model_channels=32, out_channels=3,
+               num_res_blocks=1, attention_resolutions=(2,), channel_mult=(1, 2), dims=3,
+               audio_feature_dim=64, projected_audio_dim=16, im_cond_output_ch=16, dropout=0.0)
+    m = UNetAudio(**cfg, audio_encoder=False)
+    P = _load(m, 5)
+    m = m.to(dev)
+    image = seeded((2, 3, 4, 16, 16), 1, "uniform")
+    cond = seeded((2, 3, 8, 8), 2, "uniform")
+    feat = seeded((8, 64), 3)
+    t = torch.tensor([3, 70])
+    y = m(image.to(dev), cond.to(dev), feat.to(dev), t.to(dev))
+    plan = build_plan(in_channels=3 + 16 + 16, model_channels=32, out_channels=3,
+                      num_res_blocks=1, attention_resolutions=(2,), channel_mult=(1, 2), dims=3)
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    from oracle.unet import audio_conditioned_input
+    xin = audio_conditioned_input(Pr, image, cond, feat, 16)
+    yr = unet_forward(Pr, plan, xin, t)
+    assert rel_l2(y, yr) < 1e-4
+    gy = seeded(yr.shape, 4)
+    yr.backward(gy)
+    y.backward(gy.to(dev))
+    named = dict(m.named_parameters())
+    for k in ("cond_conv_in.weight", "audio_transformer.transform.0.weight",
+              "input_blocks.0.0.weight"):
+        assert rel_l2(named[k].grad, Pr[k].grad) < 1e-4, k
+
+
+@pytest.mark.parametrize("mode", ["spatial", "temporal"])
+def test_factorised_attention_modes_vs_oracle(mode):
+    from vdiff.nn import UNetModel
+    cfg = dict(TINY3D)
+    m = UNetModel(image_size=32, **cfg, attention_mode=mode)
+    P = _load(m, 9)
+    m = m.to(dev).eval()
+    x = seeded((1, 35, 4, 32, 32), 10, "uniform")
+    t = torch.tensor([11])
+    y = m(x.to(dev), t.to(dev))
+    yr = unet_forward(P, build_plan(**cfg), x, t, attn_mode=mode)
+    assert rel_l2(y, yr) < 1e-4
+
+
+def test_spatial_temporal_block_composes_modes():
+    from vdiff.nn import AttentionBlock
+    ab = AttentionBlock(64, attention_mode="spatial_temporal")
+    P = _load(ab, 12)
+    ab = ab.to(dev)
+    x = seeded((1, 64, 3, 6, 6), 13)
+    y = ab(x.to(dev))
+    h = onn.attention_block(P, "", x, mode="spatial")
+    Pt = {"norm.weight": P["temporal_norm.weight"], "norm.bias": P["temporal_norm.bias"],
+          "qkv.weight": P["temporal_qkv.weight"], "qkv.bias": P["temporal_qkv.bias"],
+          "proj_out.weight": P["temporal_proj_out.weight"],
+          "proj_out.bias": P["temporal_proj_out.bias"]}
+    yr = onn.attention_block(Pt, "", h, mode="temporal")
+    assert rel_l2(y, yr) < 1e-5
+
+
+def test_fused_dropout_mask_consistency():
+    """Train-mode dropout fused into GN+SiLU: keep rate ~ 1-p and the backward uses the
+    same mask as the forward."""
+    from vdiff import ops
+    p = 0.25
+    x = seeded((2, 64, 4, 16, 16), 14)
+    w, b = 1 + 0.1 * seeded((64,), 15), 0.1 * seeded((64,), 16)
+    xd = ops.to_cl(x.to(dev)).requires_grad_(True)
+    y = ops.group_norm_silu(xd, w.to(dev), b.to(dev), dropout=p, seed=1234)
+    base = onn.group_norm(x, w, b, silu=True)
+    mask = (y.detach().cpu() != 0).float()
+    keep = mask.mean().item()
+    assert abs(keep - (1 - p)) < 0.01
+    assert rel_l2(y, base * mask / (1 - p)) < 1e-5
+    g = seeded(x.shape, 17)
+    y.backward(ops.to_cl(g.to(dev)))
+    xr = x.clone().requires_grad_(True)
+    (onn.group_norm(xr, w, b, silu=True) * mask / (1 - p)).backward(g)
+    assert rel_l2(xd.grad, xr.grad) < 1e-5
+    y2 = ops.group_norm_silu(xd.detach(), w.to(dev), b.to(dev), dropout=p, seed=1234)
+    assert torch.equal(y.detach(), y2)
+
+
+def test_schedulers_module_api():
+    from vdiff.schedulers import (CosineNoiseScheduler, DDIMSampler, LinearNoiseScheduler,
+                                  LinearNoiseSchedulerV2)
+    from oracle import schedulers as osch
+    s = LinearNoiseScheduler(100, 0.00085, 0.012)
+    ref = osch.linear_tables(100, 0.00085, 0.012)
+    assert torch.equal(s.alpha_cum_prod, ref["acp"])
+    x0, eps = seeded((2, 3, 4, 8, 8), 1), seeded((2, 3, 4, 8, 8), 2)
+    t = torch.tensor([5, 90])
+    out = s.add_noise(x0.to(dev), eps.to(dev), t.to(dev))
+    assert rel_l2(out, osch.q_sample(ref, x0, eps, t)) < 1e-6
+    v2 = LinearNoiseSchedulerV2(500, 0.00005, 0.015)
+    z = seeded(x0.shape, 3)
+    prev, x0p = v2.sample_prev_timestep(x0.to(dev), eps.to(dev), t.to(dev), z=z.to(dev))
+    rp, rx = osch.p_sample_v2(osch.linear_tables(500, 0.00005, 0.015), x0, eps, t, z)
+    assert rel_l2(prev, rp) < 1e-6 and rel_l2(x0p, rx) < 1e-6
+    c = CosineNoiseScheduler(2000)
+    assert torch.equal(c.alphas_cumprod, osch.cosine_tables(2000)["acp"])
+    ddim = DDIMSampler(v2, steps=50)
+    assert ddim.timesteps[0] == 499 and ddim.timesteps[-1] == 0
+    xp, _ = ddim.step(x0.to(dev), eps.to(dev), 0)
+    rxp, _ = osch.ddim_step(v2.alpha_cum_prod, x0, eps, torch.tensor([499, 499]),
+                            torch.tensor([int(ddim.prev_timesteps[0])] * 2))
+    assert rel_l2(xp, rxp) < 1e-5
