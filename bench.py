@@ -1,0 +1,308 @@
+#!/usr/bin/env python3
+"""Benchmark: train-step frames/sec + DDIM steps/sec, 128x128x16 UNet3D (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+             --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+Workload (BASELINE config 2/3): the audio + reference-image conditioned UNet3D of
+train.py:88-97 with dims=3 (model_channels 64, mult (1,2,4), 2 res blocks,
+attention at every level, 1 head, 195 input channels), joint attention over all
+T*H*W tokens (the reference semantics), bf16 activations / fp32 master weights,
+dropout 0.1 in train mode, random-init wav2vec2-base audio encoder (trainable, as
+the reference), Adam lr 1e-2.  One synthetic clip [1, 3, 16, 128, 128] (+16 audio
+windows of 4000 samples) per GPU, resident in HBM before timing.  A step = q_sample
++ forward + MSE + backward + RCCL gradient all-reduce + Adam.  Weak scaling.
+
+Secondary: DDIM steps/sec = one 50-step-DDIM denoising step (UNet forward at
+B=1 + DDIM update) on the same model, audio encoded once per clip.
+
+roofline: the flash-attention kernel with the largest share of the timed train
+step, timed per launch with HIP events on its launch stream; FLOP per launch is
+the algorithmic count (vdiff.flops.attention_kernel_flops); peak = 2.5 PF/s bf16
+dense (MI355X_MICROARCH.md).  traffic: HBM bytes per launch from the committed
+rocprofv3 PMC summary (profiles/pmc_traffic.json) if present, else null.
+cpu_baseline: the oracle (fp32 torch-CPU restatement of the reference) train step
+on a bounded sample, scaled by algorithmic FLOP to the workload (see "sample").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lipreading-video-generation_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0
+PEAK_F32_TFLOPS = 157.3
+METRIC = "train-step frames/sec + DDIM steps/sec, 128x128x16 UNet3D at 1/2/4/8 GPUs"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--size", type=int, default=128)
+    ap.add_argument("--clips-per-gpu", type=int, default=1)
+    ap.add_argument("--mode", default="joint",
+                    choices=["joint", "spatial", "temporal", "spatial_temporal"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--ddim-steps", type=int, default=None, help="timed DDIM steps (default: --steps)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-size", type=int, default=32)
+    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--only", choices=["train", "ddim", "all"], default="all")
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def build_model(args, device):
+    from vdiff.engine import reinit_nonzero
+    from vdiff.unet_audio import UNetAudio
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        model = UNetAudio(image_size=args.size, in_channels=3, model_channels=64, out_channels=3,
+                          num_res_blocks=2, attention_resolutions=(1, 2, 4),
+                          audio_feature_dim=768, projected_audio_dim=128, dims=3,
+                          use_bf16=args.dtype == "bf16", attention_mode=args.mode,
+                          audio_encoder_pretrained=False)
+    reinit_nonzero(model, seed=1234)
+    return model.to(device)
+
+
+def barrier_sync(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, device):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pick_roofline(summary, dtype):
+    """Kernel with the largest total time -> roofline object + per-kernel table."""
+    from vdiff.flops import attention_kernel_flops
+    peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
+    rows = []
+    for (kind, hd, n, nseq), (cnt, tot_ms) in summary.items():
+        f = attention_kernel_flops(kind, n, hd, nseq)
+        avg_s = tot_ms / cnt / 1e3
+        rows.append({"kernel": kind, "head_dim": hd, "seq_len": n, "nseq": nseq, "launches": cnt,
+                     "total_ms": round(tot_ms, 3), "avg_ms": round(tot_ms / cnt, 4),
+                     "tflop_per_launch": round(f / 1e12, 4),
+                     "tflops": round(f / avg_s / 1e12, 1),
+                     "frac": round(f / avg_s / 1e12 / peak, 4)})
+    rows.sort(key=lambda r: -r["total_ms"])
+    if not rows:
+        return None, rows
+    top = rows[0]
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                tab = json.load(f)
+            key = f"{top['kernel']}_d{top['head_dim']}"
+            if key in tab:
+                traffic = tab[key].get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    roof = {"bound": "mfma", "achieved": top["tflops"], "peak": peak, "unit": "TFLOP/s",
+            "frac": top["frac"], "traffic": traffic,
+            "kernel": f"{top['kernel']} (head_dim {top['head_dim']}, seq {top['seq_len']}, "
+                      f"{top['nseq']} seq/launch)",
+            "flop_per_launch": top["tflop_per_launch"] * 1e12, "avg_launch_ms": top["avg_ms"]}
+    return roof, rows
+
+
+def cpu_baseline(args, target_frames_flops):
+    """Oracle fp32 train step on a bounded sample (full-width UNet3D, joint attention,
+    reduced clip), scaled to the workload by algorithmic FLOP."""
+    import torch.nn.functional as F
+    from oracle.fixtures import FULL3D, seeded
+    from oracle.unet import (audio_conditioned_input, audio_param_shapes, build_plan,
+                             init_params, param_shapes, unet_forward)
+    from oracle import schedulers as osch
+    from vdiff.flops import unet_forward_work
+    from vdiff.nn import UNetModel
+
+    threads = torch.get_num_threads()
+    s, T = args.cpu_size, args.cpu_frames
+    plan = build_plan(**FULL3D)
+    P = init_params(param_shapes(plan), 1234)
+    P.update(init_params(audio_param_shapes(768, 128), 77))
+    for v in P.values():
+        v.requires_grad_(True)
+    tab = osch.linear_tables(100, 0.00085, 0.012)
+    x0 = seeded((1, 3, T, s, s), 0, "uniform")
+    cond = seeded((1, 3, s, s), 1, "uniform")
+    eps = seeded((1, 3, T, s, s), 2)
+    feat = seeded((T, 768), 3)
+    t = torch.tensor([37])
+    opt = torch.optim.Adam(list(P.values()), lr=1e-2)
+
+    def step():
+        xt = osch.q_sample(tab, x0, eps, t)
+        x = audio_conditioned_input(P, xt, cond, feat, 128)
+        loss = F.mse_loss(unet_forward(P, plan, x, t), eps)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+
+    step()  # warm
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el > 10.0 or n >= 3:
+            break
+    sample_fps = n * T / el
+    with torch.device("meta"):
+        m = UNetModel(image_size=s, **FULL3D)
+    f_sample = unet_forward_work(m, (1, 195, T, s, s)).total / T
+    scaled = sample_fps * f_sample / target_frames_flops
+    return {"value": scaled, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle fp32 train step (q_sample+fwd+MSE+bwd+Adam, wav2vec2 excluded), "
+                       f"full-width UNet3D joint attention at {s}x{s}x{T}, B=1: "
+                       f"{sample_fps:.3f} frames/s measured over {n} steps ({el:.1f} s), "
+                       f"scaled by algorithmic fwd FLOP/frame "
+                       f"{f_sample / 1e9:.1f} GF -> {target_frames_flops / 1e9:.1f} GF")}
+
+
+def main():
+    args = parse()
+    from vdiff import ops
+    from vdiff.ddp import broadcast_parameters, init_from_env
+    from vdiff.engine import Trainer, synthetic_clip
+    from vdiff.flops import unet_forward_work
+    from vdiff.schedulers import DDIMSampler, LinearNoiseScheduler, LinearNoiseSchedulerV2
+
+    rank, world, local = init_from_env()
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    torch.manual_seed(1234 + rank)
+
+    model = build_model(args, device)
+    broadcast_parameters(model)
+    nparams = sum(p.numel() for p in model.parameters())
+    in_shape = (args.clips_per_gpu, 195, args.frames, args.size, args.size)
+    work = unet_forward_work(model, in_shape)
+    frames_per_gpu = args.clips_per_gpu * args.frames
+    log(f"world {world}; params {nparams / 1e6:.1f} M; fwd {work.total / 1e12:.2f} TFLOP/clip "
+        f"(conv {work.conv / 1e12:.2f}, attn {work.attn / 1e12:.2f})")
+
+    result = {"metric": METRIC, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": args.dtype,
+              "data": "synthetic (seeded U[-1,1] frames / N(0,1) noise and audio), random-init "
+                      "weights incl. wav2vec2-base"}
+
+    sched = LinearNoiseScheduler(100, 0.00085, 0.012)  # train.py:48-52
+    rows = []
+    if args.only in ("train", "all"):
+        trainer = Trainer(model, sched, lr=1e-2)
+        clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
+        for i in range(args.warmup):
+            loss = trainer.step(clip)
+            log(f"warmup {i}: loss {float(loss):.4f}")
+        barrier_sync(world)
+        timer = ops.KernelTimer()
+        ops.set_timer(timer)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = trainer.step(clip)
+        barrier_sync(world)
+        el = time.perf_counter() - t0
+        ops.set_timer(None)
+        el = max_over_ranks(el, world, device)
+        ms = el / args.steps * 1e3
+        result["value"] = round(world * frames_per_gpu * args.steps / el, 4)
+        result["ms_per_step"] = round(ms, 2)
+        summary = timer.summary()
+        roof, rows = pick_roofline(summary, args.dtype)
+        result["roofline"] = roof
+        step_flops = 3 * work.total * args.clips_per_gpu
+        result["model_tflops_per_gpu"] = round(step_flops / (el / args.steps) / 1e12, 1)
+        log(f"train: {ms:.1f} ms/step, {result['value']:.3f} frames/s, loss {float(loss):.4f}, "
+            f"model {result['model_tflops_per_gpu']} TFLOP/s/GPU (3x fwd)")
+        for r in rows:
+            log("  kernel", r)
+        del trainer
+        torch.cuda.empty_cache()
+
+    if args.only in ("ddim", "all"):
+        kd = args.ddim_steps or args.steps
+        sampler = DDIMSampler(LinearNoiseSchedulerV2(500, 0.00005, 0.015), steps=50)
+        clip = synthetic_clip(1, args.frames, args.size, 500, device, seed=100 + rank)
+        model.eval()
+        with torch.no_grad():
+            feats = model.encode_audio(clip.audio)
+            xt = torch.randn_like(clip.x0)
+            for i in range(1):
+                t = torch.full((1,), int(sampler.timesteps[i]), dtype=torch.int64, device=device)
+                xt, _ = sampler.step(xt, model(xt, clip.cond, feats, t), i)
+            barrier_sync(world)
+            t0 = time.perf_counter()
+            for i in range(1, 1 + kd):
+                t = torch.full((1,), int(sampler.timesteps[i]), dtype=torch.int64, device=device)
+                xt, _ = sampler.step(xt, model(xt, clip.cond, feats, t), i)
+            barrier_sync(world)
+            el = max_over_ranks(time.perf_counter() - t0, world, device)
+        ddim = {"metric": "DDIM steps/sec (50-step DDIM, B=1 clip, replicas)",
+                "value": round(world * kd / el, 4), "unit": "steps/s",
+                "ms_per_step": round(el / kd * 1e3, 2),
+                "model_tflops_per_gpu": round(work.total / (el / kd) / 1e12, 1)}
+        result["ddim"] = ddim
+        log(f"ddim: {ddim['ms_per_step']} ms/step, {ddim['value']} steps/s")
+        if "value" not in result:
+            result.update(value=ddim["value"], unit="steps/s", ms_per_step=ddim["ms_per_step"])
+
+    result["config"] = {
+        "workload": f"train step, audio-conditioned UNet3D {args.size}x{args.size}x{args.frames} "
+                    f"({args.mode} attention), {args.clips_per_gpu} clip/GPU",
+        "clip": [args.clips_per_gpu, 3, args.frames, args.size, args.size],
+        "global_batch_clips": world * args.clips_per_gpu,
+        "attention_mode": args.mode, "parallelism": f"dp{world}",
+        "fwd_tflop_per_clip": round(work.total / 1e12, 3)}
+    if rows:
+        result["kernels"] = rows
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            result["cpu_baseline"] = cpu_baseline(args, work.total / args.frames)
+        except Exception as e:  # never let the baseline leg kill the GPU numbers
+            result["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

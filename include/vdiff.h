@@ -214,6 +214,16 @@ int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k,
                      const void* v, const void* o, const void* dout,
                      const float* lse, void* dq, void* dk, void* dv,
                      void* workspace, void* stream);
+/* The two halves of vd_attention_bwd (same arguments), for per-kernel timing:
+ * _dq writes delta = rowsum(dO * O) into the workspace and computes dq;
+ * _dkdv reads that delta and computes dk, dv.  Call _dq first. */
+int vd_attention_bwd_dq(const vd_attn_desc* d, const void* q, const void* k,
+                        const void* v, const void* o, const void* dout,
+                        const float* lse, void* dq, void* workspace,
+                        void* stream);
+int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k,
+                          const void* v, const void* dout, const float* lse,
+                          void* dk, void* dv, void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

@@ -521,9 +521,8 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
 }
 
 template <typename T, int D>
-int bwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, const void* o,
-             const void* dout, const float* lse, void* dq, void* dk, void* dv, void* ws,
-             hipStream_t st) {
+int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, const void* o,
+                const void* dout, const float* lse, void* dq, void* ws, hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   float* delta = reinterpret_cast<float*>(ws);
@@ -534,30 +533,35 @@ int bwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                                               d->seq_len, oa, d->o_token_stride);
   int rc = vd::check_launch("attn_delta");
   if (rc) return rc;
-  {
-    const size_t lds = (size_t)kStages<T> * 2 * tile_elems<T, D>() * sizeof(T);
-    auto kern = attn_bwd_dq_kernel<T, D>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq);
-    kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
-                                      delta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
-                                      d->o_token_stride, d->scale);
-    rc = vd::check_launch("attn_bwd_dq");
-    if (rc) return rc;
-  }
-  {
-    constexpr int DO = D > 128 ? 128 : D;
-    const size_t lds = (size_t)kStages<T> * 2 * tile_elems<T, D>() * sizeof(T) +
-                       (size_t)kStages<T> * 128 * sizeof(float);
-    auto kern = attn_bwd_dkdv_kernel<T, D, DO>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq, D / DO);
-    kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
-                                      delta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
-                                      d->o_token_stride, d->scale);
-    rc = vd::check_launch("attn_bwd_dkdv");
-  }
-  return rc;
+  const size_t lds = (size_t)kStages<T> * 2 * tile_elems<T, D>() * sizeof(T);
+  auto kern = attn_bwd_dq_kernel<T, D>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq);
+  kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
+                                    delta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
+                                    d->o_token_stride, d->scale);
+  return vd::check_launch("attn_bwd_dq");
+}
+
+template <typename T, int D>
+int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                  const void* dout, const float* lse, void* dk, void* dv, void* ws,
+                  hipStream_t st) {
+  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+  const float* delta = reinterpret_cast<const float*>(ws);
+  constexpr int DO = D > 128 ? 128 : D;
+  const size_t lds = (size_t)kStages<T> * 2 * tile_elems<T, D>() * sizeof(T) +
+                     (size_t)kStages<T> * 128 * sizeof(float);
+  auto kern = attn_bwd_dkdv_kernel<T, D, DO>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq, D / DO);
+  kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
+                                    delta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
+                                    d->o_token_stride, d->scale);
+  return vd::check_launch("attn_bwd_dkdv");
 }
 
 #define VD_DISPATCH_HEAD(D_, FN, ...)                        \
@@ -594,21 +598,46 @@ size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d) {
   return (size_t)d->nseq * d->seq_len * sizeof(float) + 256;
 }
 
-int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                     const void* o, const void* dout, const float* lse, void* dq, void* dk,
-                     void* dv, void* workspace, void* stream) {
+int vd_attention_bwd_dq(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                        const void* o, const void* dout, const float* lse, void* dq,
+                        void* workspace, void* stream) {
   int rc = check_attn(d);
   if (rc) return rc;
-  VD_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv && workspace, "null tensor");
+  VD_REQUIRE(q && k && v && o && dout && lse && dq && workspace, "null tensor");
   hipStream_t st = VD_STREAM(stream);
   if (d->dtype == VD_BF16) {
     using T = bf16_t;
-    VD_DISPATCH_HEAD(d->head_dim, bwd_impl, d, q, k, v, o, dout, lse, dq, dk, dv, workspace, st);
+    VD_DISPATCH_HEAD(d->head_dim, bwd_dq_impl, d, q, k, v, o, dout, lse, dq, workspace, st);
   } else if (d->dtype == VD_F32) {
     using T = float;
-    VD_DISPATCH_HEAD(d->head_dim, bwd_impl, d, q, k, v, o, dout, lse, dq, dk, dv, workspace, st);
+    VD_DISPATCH_HEAD(d->head_dim, bwd_dq_impl, d, q, k, v, o, dout, lse, dq, workspace, st);
   }
   return vd::fail(VD_EUNSUPPORTED, "dtype %d", d->dtype);
+}
+
+int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                          const void* dout, const float* lse, void* dk, void* dv, void* workspace,
+                          void* stream) {
+  int rc = check_attn(d);
+  if (rc) return rc;
+  VD_REQUIRE(q && k && v && dout && lse && dk && dv && workspace, "null tensor");
+  hipStream_t st = VD_STREAM(stream);
+  if (d->dtype == VD_BF16) {
+    using T = bf16_t;
+    VD_DISPATCH_HEAD(d->head_dim, bwd_dkdv_impl, d, q, k, v, dout, lse, dk, dv, workspace, st);
+  } else if (d->dtype == VD_F32) {
+    using T = float;
+    VD_DISPATCH_HEAD(d->head_dim, bwd_dkdv_impl, d, q, k, v, dout, lse, dk, dv, workspace, st);
+  }
+  return vd::fail(VD_EUNSUPPORTED, "dtype %d", d->dtype);
+}
+
+int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                     const void* o, const void* dout, const float* lse, void* dq, void* dk,
+                     void* dv, void* workspace, void* stream) {
+  int rc = vd_attention_bwd_dq(d, q, k, v, o, dout, lse, dq, workspace, stream);
+  if (rc) return rc;
+  return vd_attention_bwd_dkdv(d, q, k, v, dout, lse, dk, dv, workspace, stream);
 }
 
 }  // extern "C"

@@ -67,6 +67,10 @@ _SIGS = {
     "vd_attention_bwd_workspace_size": (_sz, [C.POINTER(AttnDesc)]),
     "vd_attention_bwd": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                               _vp, _vp]),
+    "vd_attention_bwd_dq": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                 _vp]),
+    "vd_attention_bwd_dkdv": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

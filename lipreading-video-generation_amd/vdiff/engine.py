@@ -1,0 +1,122 @@
+"""Training step and samplers around the drop-in model (the loops of the reference
+train.py:107-134 and test.py:51-83), plus synthetic clip generation.
+
+Differences from the reference loops (all deliberate):
+  * t ~ U{0, ..., num_timesteps-1}: the reference draws randint(0, 500) against a
+    100-step schedule (train.py:125) and crashes;
+  * no per-step torch.cuda.empty_cache() in sampling (test.py:58), and the audio
+    encoder runs once per clip instead of at every denoising step;
+  * gradients are averaged across ranks by vdiff.ddp.GradBucketer (world > 1).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .ddp import GradBucketer
+
+
+@dataclass
+class Clip:
+    """One synthetic minibatch: target frames, reference image, audio windows, noise, t."""
+    x0: torch.Tensor      # [B, 3, T, H, W] (or [B, 3, H, W])
+    cond: torch.Tensor    # [B, 3, H, W]
+    audio: dict           # {'input_values': [B*T, samples]}
+    eps: torch.Tensor     # like x0
+    t: torch.Tensor       # [B] int64
+
+
+def synthetic_clip(batch, frames, size, num_timesteps, device, seed=0, samples=4000,
+                   dims=3) -> Clip:
+    """Seeded synthetic inputs: x0, cond ~ U[-1, 1]; eps ~ N(0, 1);
+    audio ~ N(0, 1) [B*T, 4000]; t ~ U{0..N-1}.  Generated on the device."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    shape = (batch, 3, frames, size, size) if dims == 3 else (batch, 3, size, size)
+    x0 = torch.rand(shape, generator=g, device=device) * 2 - 1
+    cond = torch.rand((batch, 3, size, size), generator=g, device=device) * 2 - 1
+    eps = torch.randn(shape, generator=g, device=device)
+    nwin = batch * (frames if dims == 3 else 1)
+    audio = {"input_values": torch.randn((nwin, samples), generator=g, device=device)}
+    t = torch.randint(0, num_timesteps, (batch,), generator=g, device=device)
+    return Clip(x0, cond, audio, eps, t)
+
+
+def reinit_nonzero(model, seed=1234, std=0.02):
+    """Product-side deterministic init for benchmarks / smoke runs: the reference's
+    zero_module layers (unet.py:222-224, 306, 627) would make the denoiser output 0."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if name.startswith("audio_encoder."):
+                continue
+            if p.dim() >= 2 and float(p.detach().abs().max()) == 0.0:
+                fan_in = math.prod(p.shape[1:])
+                p.copy_(torch.randn(p.shape, generator=g) / math.sqrt(fan_in))
+            elif p.dim() == 1 and float(p.detach().abs().max()) == 0.0 and name.endswith("bias"):
+                p.copy_(std * torch.randn(p.shape, generator=g))
+    return model
+
+
+class Trainer:
+    """q_sample -> denoiser -> MSE(eps_pred, eps) -> backward -> all-reduce -> Adam.
+
+    train.py:102-103: Adam(model.parameters(), lr=1e-2), MSELoss."""
+
+    def __init__(self, model, scheduler, lr=1e-2, bucket_mb=25.0, fused_adam=True):
+        self.model = model
+        self.scheduler = scheduler
+        params = [p for p in model.parameters() if p.requires_grad]
+        self.bucketer = GradBucketer(params, bucket_mb)
+        kw = {"fused": True} if fused_adam and params and params[0].is_cuda else {}
+        self.opt = torch.optim.Adam(params, lr=lr, **kw)
+
+    def step(self, clip: Clip) -> torch.Tensor:
+        self.model.train()
+        xt = self.scheduler.add_noise(clip.x0, clip.eps, clip.t)
+        pred = self.model(xt, clip.cond, clip.audio, clip.t)
+        loss = F.mse_loss(pred, clip.eps)
+        loss.backward()
+        self.bucketer.finish()
+        self.opt.step()
+        self.bucketer.zero_grad()
+        return loss.detach()
+
+
+@torch.no_grad()
+def sample_ddim(model, sampler, cond, audio, shape, generator=None, callback=None):
+    """DDIM sampling (build extension of test.py:51-83): audio encoded once."""
+    model.eval()
+    device = cond.device
+    feats = model.encode_audio(audio) if hasattr(model, "encode_audio") else audio
+    xt = torch.randn(shape, generator=generator, device=device)
+    x0 = None
+    for i in range(sampler.steps):
+        t = torch.full((shape[0],), int(sampler.timesteps[i]), dtype=torch.int64, device=device)
+        eps = model(xt, cond, feats, t)
+        xt, x0 = sampler.step(xt, eps, i)
+        if callback is not None:
+            callback(i, xt, x0)
+    return xt, x0
+
+
+@torch.no_grad()
+def sample_ddpm(model, scheduler, cond, audio, shape, n_timesteps=None, generator=None,
+                callback=None):
+    """Ancestral sampling as test.py:51-83 (V2 scheduler by default there)."""
+    model.eval()
+    device = cond.device
+    feats = model.encode_audio(audio) if hasattr(model, "encode_audio") else audio
+    n = n_timesteps or scheduler.num_timesteps
+    xt = torch.randn(shape, generator=generator, device=device)
+    x0 = None
+    for i in reversed(range(n)):
+        t = torch.full((shape[0],), i, dtype=torch.int64, device=device)
+        eps = model(xt, cond, feats, t)
+        z = torch.randn(xt.shape, generator=generator, device=device)
+        xt, x0 = scheduler.sample_prev_timestep(xt, eps, t, z=z)
+        if callback is not None:
+            callback(i, xt, x0)
+    return xt, x0

@@ -1,0 +1,97 @@
+"""Analytic algorithmic work of the denoiser (the denominators of roofline.achieved).
+
+Counts follow torch.utils.flop_counter conventions on the reference modules (2 FLOP
+per MAC): conv = 2*B*out_pixels*Co*Ci*taps; attention = 2 bmm per block =
+4*B*heads*N^2*ch (joint), per-frame N = H*W (spatial) or per-pixel N = T (temporal).
+Linear layers and elementwise work are not counted.
+The training step is counted as 3 x forward (no credit for recompute).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+
+@dataclass
+class Work:
+    conv: float = 0.0
+    attn: float = 0.0
+    attn_by_dim: dict = field(default_factory=dict)  # head_dim -> (fwd FLOP, launches, N, nseq)
+
+    @property
+    def total(self):
+        return self.conv + self.attn
+
+
+def _conv(w: Work, B, pix, co, ci, taps):
+    w.conv += 2.0 * B * pix * co * ci * taps
+
+
+def _attn(w: Work, B, C, heads, T, HW, mode):
+    ch = C // heads
+    modes = ["spatial", "temporal"] if mode == "spatial_temporal" else [mode]
+    for md in modes:
+        if md == "joint":
+            nseq, n = B * heads, T * HW
+        elif md == "spatial":
+            nseq, n = B * heads * T, HW
+        else:
+            nseq, n = B * heads * HW, T
+        f = 4.0 * nseq * n * n * ch
+        w.attn += f
+        prev = w.attn_by_dim.get((ch, n), (0.0, 0, n, nseq))
+        w.attn_by_dim[(ch, n)] = (prev[0] + f, prev[1] + 1, n, nseq)
+        # qkv / proj 1x1 convs per sub-attention
+        _conv(w, B, T * HW, 3 * C, C, 1)
+        _conv(w, B, T * HW, C, C, 1)
+
+
+def unet_forward_work(model, x_shape) -> Work:
+    """Walk a vdiff UNetModel for input shape [B, Cin, (T,) H, W]."""
+    from .nn import AttentionBlock, Downsample, ResBlock, Upsample
+
+    B = x_shape[0]
+    if len(x_shape) == 5:
+        T, H, W = x_shape[2:]
+    else:
+        T, (H, W) = 1, x_shape[2:]
+    w = Work()
+    k = 27 if model.dims == 3 else 9
+    state = {"H": H, "W": W}
+
+    def block(seq):
+        for layer in seq:
+            pix = T * state["H"] * state["W"]
+            if isinstance(layer, ResBlock):
+                _conv(w, B, pix, layer.out_channels, layer.channels, k)
+                _conv(w, B, pix, layer.out_channels, layer.out_channels, k)
+                if layer.out_channels != layer.channels:
+                    _conv(w, B, pix, layer.out_channels, layer.channels, 1)
+            elif isinstance(layer, AttentionBlock):
+                _attn(w, B, layer.channels, layer.num_heads, T, state["H"] * state["W"],
+                      layer.attention_mode)
+            elif isinstance(layer, Downsample):
+                state["H"] = (state["H"] + 1) // 2
+                state["W"] = (state["W"] + 1) // 2
+                _conv(w, B, T * state["H"] * state["W"], layer.out_channels, layer.channels, k)
+            elif isinstance(layer, Upsample):
+                state["H"] *= 2
+                state["W"] *= 2
+                _conv(w, B, T * state["H"] * state["W"], layer.out_channels, layer.channels, k)
+            else:  # the input conv
+                _conv(w, B, pix, layer.out_channels, layer.in_channels, k)
+
+    for m in model.input_blocks:
+        block(m)
+    block(model.middle_block)
+    for m in model.output_blocks:
+        block(m)
+    _conv(w, B, T * H * W, model.out_channels, model.out[2].in_channels, k)
+    return w
+
+
+def attention_kernel_flops(kind: str, n: int, ch: int, nseq: int) -> float:
+    """Algorithmic FLOP of one launch of a flash-attention kernel:
+    fwd = 2 products (QK^T, PV); bwd dQ = 3 (QK^T, dO V^T, dS K);
+    bwd dK/dV = 4 (QK^T, dO V^T, dO^T P, dS^T Q).  Each product = 2*n*n*ch per sequence."""
+    products = {"fwd": 2, "bwd_dq": 3, "bwd_dkdv": 4}[kind.replace("attn_", "")]
+    return products * 2.0 * nseq * n * n * ch

@@ -441,6 +441,45 @@ def conv(x, weight, bias=None, stride=1, padding=0, chan_add=None, residual=None
 
 
 # --------------------------------------------------------------- Attention
+class KernelTimer:
+    """HIP-event timing of every flash-attention launch on the launching (current) stream.
+
+    bench.py installs one over its timed region: vdiff.ops.set_timer(KernelTimer()).
+    Each record is (kind, head_dim, seq_len, nseq, start_event, end_event)."""
+
+    def __init__(self):
+        self.records = []
+
+    def begin(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def end(self, start, kind, d):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.records.append((kind, d.head_dim, d.seq_len, d.nseq, start, e))
+
+    def summary(self):
+        """{(kind, head_dim, seq_len, nseq): [count, total_ms]} (synchronizes)."""
+        torch.cuda.synchronize()
+        out = {}
+        for kind, hd, n, nseq, s, e in self.records:
+            k = (kind, hd, n, nseq)
+            c = out.setdefault(k, [0, 0.0])
+            c[0] += 1
+            c[1] += s.elapsed_time(e)
+        return out
+
+
+_timer = None
+
+
+def set_timer(timer):
+    global _timer
+    _timer = timer
+
+
 def _attn_desc(B, N, C, heads, ch, mode, spatial, dtype, legacy):
     """Descriptor(s) for the q/k/v views of a [B][N][3C] qkv buffer.
 
@@ -492,8 +531,11 @@ class AttentionFn(torch.autograd.Function):
         for d, qo, ko, vo, oo in launches:
             lse = torch.empty(d.nseq * d.seq_len, dtype=torch.float32, device=qkv.device)
             base = qkv.data_ptr()
+            ev = _timer.begin() if _timer is not None else None
             _lib.call("vd_attention_fwd", d, base + qo * es, base + ko * es, base + vo * es,
                       out.data_ptr() + oo * es, _p(lse), _stream(qkv))
+            if ev is not None:
+                _timer.end(ev, "attn_fwd", d)
             lses.append(lse)
         ctx.save_for_backward(qkv, out, *lses)
         ctx.cfg = (heads, mode, spatial, legacy)
@@ -515,9 +557,17 @@ class AttentionFn(torch.autograd.Function):
         for (d, qo, ko, vo, oo), lse in zip(launches, lses):
             ws = torch.empty(max(1, _lib.lib().vd_attention_bwd_workspace_size(d)),
                              dtype=torch.uint8, device=qkv.device)
-            _lib.call("vd_attention_bwd", d, base + qo * es, base + ko * es, base + vo * es,
-                      obase + oo * es, dobase + oo * es, _p(lse), dbase + qo * es,
-                      dbase + ko * es, dbase + vo * es, _p(ws), _stream(qkv))
+            st = _stream(qkv)
+            ev = _timer.begin() if _timer is not None else None
+            _lib.call("vd_attention_bwd_dq", d, base + qo * es, base + ko * es, base + vo * es,
+                      obase + oo * es, dobase + oo * es, _p(lse), dbase + qo * es, _p(ws), st)
+            if ev is not None:
+                _timer.end(ev, "attn_bwd_dq", d)
+                ev = _timer.begin()
+            _lib.call("vd_attention_bwd_dkdv", d, base + qo * es, base + ko * es, base + vo * es,
+                      dobase + oo * es, _p(lse), dbase + ko * es, dbase + vo * es, _p(ws), st)
+            if ev is not None:
+                _timer.end(ev, "attn_bwd_dkdv", d)
         return dqkv, None, None, None, None
 
 
