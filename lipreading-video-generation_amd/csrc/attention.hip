@@ -133,16 +133,35 @@ __device__ __forceinline__ void mma_rows(f32x16& acc, const T* tile, int row0,
   }
 }
 
-__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
-}
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) { return pack2bf(a, b); }
+
+// A 32x32 accumulator X used as the B operand of a following product (its ROW
+// index, in registers, is the summed index; SS 3 of the HIP guide): bf16 packs it
+// once into two 16-deep k-step fragments, fp32 keeps the registers.
+template <typename T> struct XOp;
+template <> struct XOp<bf16_t> {
+  bf16x8 b[2];
+  __device__ __forceinline__ explicit XOp(const f32x16& X) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const uint4 w = make_uint4(pack_bf16(X[8 * s2 + 0], X[8 * s2 + 1]),
+                                 pack_bf16(X[8 * s2 + 2], X[8 * s2 + 3]),
+                                 pack_bf16(X[8 * s2 + 4], X[8 * s2 + 5]),
+                                 pack_bf16(X[8 * s2 + 6], X[8 * s2 + 7]));
+      b[s2] = __builtin_bit_cast(bf16x8, w);
+    }
+  }
+};
+template <> struct XOp<float> {
+  f32x16 x;
+  __device__ __forceinline__ explicit XOp(const f32x16& X) : x(X) {}
+};
 
 // acc[32 tile cols from col0 (rows of the result)][32 lanes] +=
-//   tile[sum0 .. sum0+32][col0 ..]^T  x  X, where X is a 32x32 accumulator whose
-// ROW index (registers) is the summed index.
+//   tile[sum0 .. sum0+32][col0 ..]^T  x  X
 template <typename T, int D>
 __device__ __forceinline__ void mma_tr(f32x16& acc, const T* tile, int sum0, int col0,
-                                       const f32x16& X, int lane) {
+                                       const XOp<T>& X, int lane) {
   const int hh = lane >> 5;
   if constexpr (sizeof(T) == 2) {
     const int g = lane >> 4, fr = lane & 15;
@@ -150,11 +169,7 @@ __device__ __forceinline__ void mma_tr(f32x16& acc, const T* tile, int sum0, int
     const int col = col0 + 16 * (g & 1) + 4 * p4;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const uint4 w = make_uint4(pack_bf16(X[8 * s2 + 0], X[8 * s2 + 1]),
-                                 pack_bf16(X[8 * s2 + 2], X[8 * s2 + 3]),
-                                 pack_bf16(X[8 * s2 + 4], X[8 * s2 + 5]),
-                                 pack_bf16(X[8 * s2 + 6], X[8 * s2 + 7]));
-      const bf16x8 bop = __builtin_bit_cast(bf16x8, w);
+      const bf16x8 bop = X.b[s2];
       const int kr = sum0 + 16 * s2 + 4 * (g >> 1) + q4;
       const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (lds_bf16x4*)(tile + toff<T, D>(kr, col)));
@@ -168,10 +183,13 @@ __device__ __forceinline__ void mma_tr(f32x16& acc, const T* tile, int sum0, int
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float a = tile[toff<T, D>(sum0 + (r & 3) + 8 * (r >> 2) + 4 * hh, c)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, X[r], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, X.x[r], acc, 0, 0, 0);
     }
   }
 }
+
+// v_exp_f32 directly (inputs here are <= 0 or -inf; no range reduction needed)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // row index (0..31) of accumulator register r for this lane half
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
@@ -206,7 +224,158 @@ struct SeqAddr {
   }
 };
 
-template <typename T> constexpr int kStages = sizeof(T) == 2 ? 2 : 1;
+
+// ------------------------------------------------------------------ tile pipelines
+// bf16: LDS ring of NST stages filled by buffer_load ... lds (LDS-DMA, no register
+// staging).  The buffer range check zero-fills rows past the sequence end.  Tile t+NST-1
+// is issued at the top of iteration t, so NST-1 tiles are in flight while tile t is
+// computed; one raw s_barrier per tile, behind a counted vmcnt (never vmcnt(0) in the
+// loop: __syncthreads() would drain the ring).
+// fp32 (parity mode): one register-staged stage (rows of D+1 floats).
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <typename T> constexpr bool kDMA = sizeof(T) == 2;
+
+template <int D> constexpr int nstage() { return D <= 64 ? 4 : (D == 128 ? 3 : 2); }
+template <int D> constexpr int dma_ipw() { return kTile * D * 2 / 1024 / 4; }  // per wave per tile
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+// this wave's share of one [64 x D] bf16 tile: logical 16-B chunk c of row r lands at the
+// swizzled position toff(r, 8c) (the DMA writes lane-linearly, so the SOURCE chunk is
+// permuted by the same involution)
+template <int D>
+__device__ __forceinline__ void dma_tile(__amdgpu_buffer_rsrc_t rs, char* lds, int tok0, int n,
+                                         uint32_t ts_bytes, int wave, int lane) {
+  constexpr int CPL = D / 8, RPI = 64 / CPL, IPW = dma_ipw<D>();
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int gi = wave * IPW + i;
+    const int row = gi * RPI + lane / CPL;
+    const int c = (lane % CPL) ^ swz_row<D>(row);
+    const int tok = tok0 + row;
+    const uint32_t voff = tok < n ? (uint32_t)tok * ts_bytes + (uint32_t)c * 16u : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + gi * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// 64 fp32 row constants (one dword per lane)
+__device__ __forceinline__ void dma_rowc(__amdgpu_buffer_rsrc_t rs, char* lds, int tok0,
+                                         int lane) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 4, (uint32_t)(tok0 + lane) * 4u, 0,
+                                           0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t seq_bytes(int n, int64_t ts, int D, int esz) {
+  return (uint32_t)(((int64_t)(n - 1) * ts + D) * esz);
+}
+
+// Runs body(t, tileA, tileB) over all 64-row tiles of two row streams (a, b) of one
+// sequence; with RC, the fp32 row constants rc0/rc1 of the tile are staged too and
+// passed as body's fourth argument (float* [rc0 64 | rc1 64]).
+template <typename T, int D, bool RC, typename Body>
+__device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, int64_t ts_a,
+                                          int64_t ts_b, const float* rc0, const float* rc1, int n,
+                                          int tid, Body&& body) {
+  constexpr int TE = tile_elems<T, D>();
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntiles = (n + kTile - 1) / kTile;
+  if constexpr (kDMA<T>) {
+    constexpr int NST = nstage<D>();
+    constexpr int STAGE_BYTES = 2 * TE * 2 + (RC ? 768 : 0);
+    constexpr int PER_TILE = 2 * dma_ipw<D>() + (RC ? 1 : 0);
+    const auto ra = make_rsrc(a, seq_bytes(n, ts_a, D, 2));
+    const auto rb = make_rsrc(b, seq_bytes(n, ts_b, D, 2));
+    __amdgpu_buffer_rsrc_t r0, r1;
+    if constexpr (RC) {
+      r0 = make_rsrc(rc0, (uint32_t)n * 4u);
+      r1 = make_rsrc(rc1, (uint32_t)n * 4u);
+    }
+    const uint32_t tsa = (uint32_t)(ts_a * 2), tsb = (uint32_t)(ts_b * 2);
+    auto issue = [&](int t) {
+      char* st = smem + (t % NST) * STAGE_BYTES;
+      const int tok0 = t * kTile;
+      dma_tile<D>(ra, st, tok0, n, tsa, wave, lane);
+      dma_tile<D>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
+      if constexpr (RC) {  // waves 0/1 stage the two constants, 2/3 a throw-away copy
+        // (every wave issues the same number of DMAs, so one vmcnt fits all)
+        char* rcs = st + 4 * TE + (wave < 2 ? wave * 256 : 512);
+        dma_rowc(wave == 1 ? r1 : r0, rcs, tok0, lane);
+      }
+    };
+    vm_drain();  // fragments loaded before the loop are in; the ring's counts start clean
+#pragma unroll
+    for (int s = 0; s < NST - 1; ++s) issue(s);
+    for (int t = 0; t < ntiles; ++t) {
+      vm_wait_barrier<(NST - 2) * PER_TILE>();
+      issue(t + NST - 1);  // beyond the end: fully out-of-range rows (zero fill, no traffic)
+      const char* st = smem + (t % NST) * STAGE_BYTES;
+      body(t, reinterpret_cast<const T*>(st), reinterpret_cast<const T*>(st + TE * 2),
+           reinterpret_cast<const float*>(st + 4 * TE));
+    }
+    vm_drain();
+  } else {
+    T* lds = reinterpret_cast<T*>(smem);
+    float* rcl = reinterpret_cast<float*>(smem + 2 * TE * sizeof(T));
+    Stager<T, D> sa, sb;
+    float v0 = 0.f, v1 = 0.f;
+    auto ldrc = [&](int tok0) {
+      if constexpr (RC) {
+        if (tid < kTile) {
+          v0 = tok0 + tid < n ? rc0[tok0 + tid] : 0.f;
+          v1 = tok0 + tid < n ? rc1[tok0 + tid] : 0.f;
+        }
+      }
+    };
+    auto strc = [&]() {
+      if constexpr (RC) {
+        if (tid < kTile) {
+          rcl[tid] = v0;
+          rcl[64 + tid] = v1;
+        }
+      }
+    };
+    sa.load(a, ts_a, 0, n, tid);
+    sb.load(b, ts_b, 0, n, tid);
+    ldrc(0);
+    sa.store(lds, tid);
+    sb.store(lds + TE, tid);
+    strc();
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+      const bool more = t + 1 < ntiles;
+      if (more) {
+        sa.load(a, ts_a, (t + 1) * kTile, n, tid);
+        sb.load(b, ts_b, (t + 1) * kTile, n, tid);
+        ldrc((t + 1) * kTile);
+      }
+      body(t, lds, lds + TE, rcl);
+      __syncthreads();
+      if (more) {
+        sa.store(lds, tid);
+        sb.store(lds + TE, tid);
+        strc();
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <typename T, int D, bool RC>
+size_t tile_loop_lds() {
+  if constexpr (kDMA<T>) return (size_t)nstage<D>() * (2 * tile_elems<T, D>() * 2 + (RC ? 768 : 0));
+  else return 2 * tile_elems<T, D>() * sizeof(T) + (RC ? 512 : 0);
+}
 
 // ================================================================== forward
 template <typename T, int D>
@@ -214,89 +383,73 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TE = tile_elems<T, D>();
-  constexpr int ST = kStages<T>;
-  T* lds = reinterpret_cast<T*>(smem);  // [ST][K, V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * kRows + wave * 32;
   const int64_t base = qa(seq);
-  const T* qb = q + base;
-  const T* kb = k + base;
-  const T* vb = v + base;
   const int myq = q0 + (lane & 31);
 
   RowFrag<T, D> qf;
-  qf.load(qb, ts, myq, n, lane);
+  qf.load(q + base, ts, myq, n, lane);
   f32x16 oacc[D / 32];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
   float m = -INFINITY, l = 0.f;
   const float c = scale * kLog2e;
 
-  Stager<T, D> sk, sv;
-  const int ntiles = (n + kTile - 1) / kTile;
-  sk.load(kb, ts, 0, n, tid);
-  sv.load(vb, ts, 0, n, tid);
-  sk.store(lds, tid);
-  sv.store(lds + TE, tid);
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  tile_loop<T, D, false>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
+                         [&](int t, const T* Kt, const T* Vt, const float*) {
     const int key0 = t * kTile;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      sk.load(kb, ts, key0 + kTile, n, tid);
-      sv.load(vb, ts, key0 + kTile, n, tid);
-    }
-    const T* Kt = lds + (t % ST) * 2 * TE;
-    const T* Vt = Kt + TE;
     f32x16 s[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       s[h] = f32x16{};
       mma_rows<T, D>(s[h], Kt, 32 * h, qf, lane);
     }
-    // online softmax in the log2 domain; keys on registers, query on the lane
-    float tmax = -INFINITY;
+    // online softmax in the log2 domain; keys on registers, query on the lane.
+    // Only the tail tile needs the key mask (wave-uniform branch).
+    if (key0 + kTile > n) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (key0 + 32 * h + acc_row(r, hh) >= n) s[h][r] = -INFINITY;
+    }
+    float tmax = s[0][0];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = key0 + 32 * h + acc_row(r, hh);
-        const float x = key < n ? s[h][r] * c : -INFINITY;
-        s[h][r] = x;
-        tmax = fmaxf(tmax, x);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mnew);
-    m = mnew;
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[h][r]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;  // c > 0: max commutes with the scale
+    // exact lazy rescale: only when some row max of this wave grew
+    if (!__all(tmax <= m)) {
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = fast_exp2(m - mnew);
+      m = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+    }
+    const float nm = -m;
     float psum = 0.f;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[h][r] - mnew);
+        const float p = fast_exp2(fmaf(s[h][r], c, nm));
         s[h][r] = p;
         psum += p;
       }
-    l = l * alpha + psum;
+    l += psum;
+    const XOp<T> p0(s[0]), p1(s[1]);
 #pragma unroll
-    for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) mma_tr<T, D>(oacc[i], Vt, 32 * h, 32 * i, s[h], lane);
-    if (ST == 1) __syncthreads();
-    if (more) {
-      T* nxt = lds + ((t + 1) % ST) * 2 * TE;
-      sk.store(nxt, tid);
-      sv.store(nxt + TE, tid);
+    for (int i = 0; i < D / 32; ++i) {
+      mma_tr<T, D>(oacc[i], Vt, 0, 32 * i, p0, lane);
+      mma_tr<T, D>(oacc[i], Vt, 32, 32 * i, p1, lane);
     }
-    __syncthreads();
-  }
+  });
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.f / l;
   store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, oacc, inv, lane);
@@ -333,10 +486,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
     const T* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     T* __restrict__ dq, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TE = tile_elems<T, D>();
-  constexpr int ST = kStages<T>;
-  T* lds = reinterpret_cast<T*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * kRows + wave * 32;
   const int64_t base = qa(seq);
@@ -346,52 +496,31 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
   RowFrag<T, D> qf, of;
   qf.load(q + base, ts, myq, n, lane);
   of.load(dout + oa(seq), ots, myq, n, lane);
-  const float lse2 = myq < n ? lse[(int64_t)seq * n + myq] * kLog2e : 0.f;
+  const float nlse2 = myq < n ? -lse[(int64_t)seq * n + myq] * kLog2e : 0.f;
   const float dlt = myq < n ? delta[(int64_t)seq * n + myq] : 0.f;
   f32x16 acc[D / 32];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) acc[i] = f32x16{};
 
-  const T* kb = k + base;
-  const T* vb = v + base;
-  Stager<T, D> sk, sv;
-  const int ntiles = (n + kTile - 1) / kTile;
-  sk.load(kb, ts, 0, n, tid);
-  sv.load(vb, ts, 0, n, tid);
-  sk.store(lds, tid);
-  sv.store(lds + TE, tid);
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int key0 = t * kTile;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      sk.load(kb, ts, key0 + kTile, n, tid);
-      sv.load(vb, ts, key0 + kTile, n, tid);
-    }
-    const T* Kt = lds + (t % ST) * 2 * TE;
-    const T* Vt = Kt + TE;
+  tile_loop<T, D, false>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
+                         [&](int, const T* Kt, const T* Vt, const float*) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x16 s = f32x16{}, dp = f32x16{};
       mma_rows<T, D>(s, Kt, 32 * h, qf, lane);
       mma_rows<T, D>(dp, Vt, 32 * h, of, lane);
+      // keys past n have zero K/V rows: their dS^T multiplies a zero K row in the
+      // dQ product, so no mask is needed here
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int key = key0 + 32 * h + acc_row(r, hh);
-        const float p = key < n ? exp2f(s[r] * c - lse2) : 0.f;
+        const float p = fast_exp2(fmaf(s[r], c, nlse2));
         s[r] = p * (dp[r] - dlt);  // dS^T
       }
+      const XOp<T> ds(s);
 #pragma unroll
-      for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(acc[i], Kt, 32 * h, 32 * i, s, lane);
+      for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(acc[i], Kt, 32 * h, 32 * i, ds, lane);
     }
-    if (ST == 1) __syncthreads();
-    if (more) {
-      T* nxt = lds + ((t + 1) % ST) * 2 * TE;
-      sk.store(nxt, tid);
-      sv.store(nxt + TE, tid);
-    }
-    __syncthreads();
-  }
+  });
   store_transposed<T, D / 32>(dq + base, ts, myq, n, 0, acc, scale, lane);
 }
 
@@ -405,10 +534,6 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     T* __restrict__ dk, T* __restrict__ dv, int n, SeqAddr qa, int64_t ts, SeqAddr oa,
     int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TE = tile_elems<T, D>();
-  constexpr int ST = kStages<T>;
-  T* lds = reinterpret_cast<T*>(smem);  // [ST][Q, dO]
-  float* rowc = reinterpret_cast<float*>(smem + (size_t)ST * 2 * TE * sizeof(T));  // [ST][2][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   const int seq = blockIdx.y;
   const int d0 = blockIdx.z * DO;
@@ -424,74 +549,38 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
   for (int i = 0; i < DO / 32; ++i) adv[i] = adk[i] = f32x16{};
 
-  const T* qb = q + base;
-  const T* ob = dout + obase;
-  const float* lrow = lse + (int64_t)seq * n;
-  const float* drow = delta + (int64_t)seq * n;
-  Stager<T, D> sq, so;
-  float rl = 0.f, rd = 0.f;
-  auto load_rows = [&](int tok0) {
-    if (tid < kTile) {
-      const int tk = tok0 + tid;
-      rl = tk < n ? lrow[tk] * kLog2e : 0.f;
-      rd = tk < n ? drow[tk] : 0.f;
-    }
-  };
-  auto store_rows = [&](int stage) {
-    if (tid < kTile) {
-      rowc[stage * 128 + tid] = rl;
-      rowc[stage * 128 + 64 + tid] = rd;
-    }
-  };
-  const int ntiles = (n + kTile - 1) / kTile;
-  sq.load(qb, ts, 0, n, tid);
-  so.load(ob, ots, 0, n, tid);
-  load_rows(0);
-  sq.store(lds, tid);
-  so.store(lds + TE, tid);
-  store_rows(0);
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int qt0 = t * kTile;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      sq.load(qb, ts, qt0 + kTile, n, tid);
-      so.load(ob, ots, qt0 + kTile, n, tid);
-      load_rows(qt0 + kTile);
-    }
-    const int stage = t % ST;
-    const T* Qt = lds + stage * 2 * TE;
-    const T* Ot = Qt + TE;
-    const float* L = rowc + stage * 128;
+  // query rows past n have zero Q / dO rows and zero lse / delta, so they add nothing
+  // to dV (dO = 0) or dK (dS = p * (0 - 0)): no mask needed.
+  tile_loop<T, D, true>(smem, q + base, dout + obase, ts, ots, lse + (int64_t)seq * n,
+                        delta + (int64_t)seq * n, n, tid,
+                        [&](int, const T* Qt, const T* Ot, const float* L) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x16 s = f32x16{}, dp = f32x16{};
       mma_rows<T, D>(s, Qt, 32 * h, kf, lane);   // S[q][key]
       mma_rows<T, D>(dp, Ot, 32 * h, vf, lane);  // dP[q][key]
+      // registers 4g..4g+3 are rows 8g + 4hh + 0..3: one b128 read per constant
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = 32 * h + acc_row(r, hh);
-        const bool ok = qt0 + ql < n && mykey < n;
-        const float p = ok ? exp2f(s[r] * c - L[ql]) : 0.f;
-        s[r] = p;
-        dp[r] = p * (dp[r] - L[64 + ql]);  // dS
+      for (int g = 0; g < 4; ++g) {
+        const float4 ls = *reinterpret_cast<const float4*>(L + 32 * h + 8 * g + 4 * hh);
+        const float4 dl = *reinterpret_cast<const float4*>(L + 64 + 32 * h + 8 * g + 4 * hh);
+        const float lv[4] = {ls.x, ls.y, ls.z, ls.w}, dlv[4] = {dl.x, dl.y, dl.z, dl.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float p = fast_exp2(fmaf(s[r], c, -lv[e] * kLog2e));
+          s[r] = p;
+          dp[r] = p * (dp[r] - dlv[e]);  // dS
+        }
       }
+      const XOp<T> pp(s), ds(dp);
 #pragma unroll
       for (int i = 0; i < DO / 32; ++i) {
-        mma_tr<T, D>(adv[i], Ot, 32 * h, d0 + 32 * i, s, lane);   // dV^T += dO^T P
-        mma_tr<T, D>(adk[i], Qt, 32 * h, d0 + 32 * i, dp, lane);  // dK^T += Q^T dS
+        mma_tr<T, D>(adv[i], Ot, 32 * h, d0 + 32 * i, pp, lane);  // dV^T += dO^T P
+        mma_tr<T, D>(adk[i], Qt, 32 * h, d0 + 32 * i, ds, lane);  // dK^T += Q^T dS
       }
     }
-    if (ST == 1) __syncthreads();
-    if (more) {
-      const int ns = (t + 1) % ST;
-      T* nxt = lds + ns * 2 * TE;
-      sq.store(nxt, tid);
-      so.store(nxt + TE, tid);
-      store_rows(ns);
-    }
-    __syncthreads();
-  }
+  });
   store_transposed<T, DO / 32>(dk + base, ts, mykey, n, d0, adk, scale, lane);
   store_transposed<T, DO / 32>(dv + base, ts, mykey, n, d0, adv, 1.f, lane);
 }
@@ -502,15 +591,21 @@ int check_attn(const vd_attn_desc* d) {
   VD_REQUIRE(d->nseq > 0 && d->seq_len > 0 && d->groups > 0, "bad attention shape");
   VD_REQUIRE(d->head_dim == 32 || d->head_dim == 64 || d->head_dim == 128 || d->head_dim == 256,
              "head_dim %d unsupported (32/64/128/256)", d->head_dim);
+  if (d->dtype == VD_BF16) {  // 32-bit buffer offsets of the LDS-DMA ring
+    VD_REQUIRE(((int64_t)d->seq_len * d->token_stride + d->head_dim) * 2 < 0x7fffffffLL &&
+                   ((int64_t)d->seq_len * d->o_token_stride + d->head_dim) * 2 < 0x7fffffffLL,
+               "sequence spans >= 2 GiB");
+  }
   return VD_OK;
 }
 
 template <typename T, int D>
 int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
              float* lse, hipStream_t st) {
-  const size_t lds = (size_t)kStages<T> * 2 * tile_elems<T, D>() * sizeof(T);
+  const size_t lds = tile_loop_lds<T, D, false>();
   auto kern = attn_fwd_kernel<T, D>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
   dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq);
   kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
                                     d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
@@ -533,7 +628,7 @@ int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void*
                                               d->seq_len, oa, d->o_token_stride);
   int rc = vd::check_launch("attn_delta");
   if (rc) return rc;
-  const size_t lds = (size_t)kStages<T> * 2 * tile_elems<T, D>() * sizeof(T);
+  const size_t lds = tile_loop_lds<T, D, false>();
   auto kern = attn_bwd_dq_kernel<T, D>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
@@ -552,8 +647,7 @@ int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const voi
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const float* delta = reinterpret_cast<const float*>(ws);
   constexpr int DO = D > 128 ? 128 : D;
-  const size_t lds = (size_t)kStages<T> * 2 * tile_elems<T, D>() * sizeof(T) +
-                     (size_t)kStages<T> * 128 * sizeof(float);
+  const size_t lds = tile_loop_lds<T, D, true>();
   auto kern = attn_bwd_dkdv_kernel<T, D, DO>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);

@@ -30,12 +30,14 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
-// round-to-nearest-even; NaN stays NaN (quiet bit forced)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+// fp32 -> bf16, round-to-nearest-even, NaN stays NaN: one v_cvt_pk_bf16_f32 on gfx950
+// (an integer-arithmetic rounding with a NaN test compiles to a divergent branch per
+// element).
+typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
+typedef float f32x2_hw __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_hw){a, b}, bf16x2_hw));
 }
 
 // Load/store N consecutive elements of T as fp32 (N*sizeof(T) must be 8 or 16 B aligned).
@@ -72,11 +74,8 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
-  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]),
+                                            pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
 }
 
 // counter-based dropout keep mask (splitmix64 of seed + idx); returns 0 or 1/(1-p)

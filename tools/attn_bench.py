@@ -1,0 +1,58 @@
+"""Micro-benchmark of the flash-attention kernels at the UNet3D 128x128x16 shapes
+(joint attention, 1 head): level 0 (d 64, N 262144), level 1 (d 128, N 65536),
+level 2 (d 256, N 16384).  Times fwd / bwd_dq / bwd_dkdv per launch with HIP
+events on the launch stream; prints TFLOP/s and fraction of the 2.5 PF/s bf16 peak.
+Also checks a small case against a materialised fp32 softmax reference."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "lipreading-video-generation_amd"))
+
+import torch  # noqa: E402
+
+from vdiff import ops  # noqa: E402
+from vdiff.flops import attention_kernel_flops  # noqa: E402
+
+
+def check():
+    torch.manual_seed(0)
+    for C, N in ((64, 300), (128, 200), (256, 130)):
+        qkv = torch.randn(1, 3 * C, N, device="cuda")
+        q, k, v = qkv.reshape(3, C, N)
+        ref = torch.softmax((q.T @ k) / C ** 0.5, -1) @ v.T
+        out = ops.attention(ops.to_cl(qkv.bfloat16()), 1)
+        e = ((out.float()[0].T - ref).norm() / ref.norm()).item()
+        print(f"check C={C} N={N}: rel-L2 {e:.2e}", flush=True)
+        assert e < 2e-2
+
+
+def bench(C, N, reps, bwd=True):
+    qkv = ops.to_cl(torch.randn(1, 3 * C, N, device="cuda", dtype=torch.bfloat16))
+    qkv.requires_grad_(True)
+    g = ops.to_cl(torch.randn(1, C, N, device="cuda", dtype=torch.bfloat16))
+    for _ in range(1):
+        out = ops.attention(qkv, 1)
+        if bwd:
+            out.backward(g)
+    torch.cuda.synchronize()
+    timer = ops.KernelTimer()
+    ops.set_timer(timer)
+    for _ in range(reps):
+        out = ops.attention(qkv, 1)
+        if bwd:
+            out.backward(g)
+    ops.set_timer(None)
+    for (kind, hd, n, nseq), (cnt, tot) in sorted(timer.summary().items()):
+        f = attention_kernel_flops(kind, n, hd, nseq)
+        avg = tot / cnt
+        print(f"{kind:14s} d={hd:3d} N={n:6d}: {avg:8.3f} ms  {f / avg / 1e9:7.1f} TF/s "
+              f"({f / avg / 1e9 / 2500 * 100:5.1f}% of 2.5 PF)", flush=True)
+
+
+if __name__ == "__main__":
+    check()
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    for C, N in ((64, 262144), (128, 65536), (256, 16384)):
+        bench(C, N, reps)
