@@ -123,27 +123,30 @@ __global__ __launch_bounds__(kThreads) void gn_stats_kernel(const T* __restrict_
   }
 }
 
-// grid B, 256 threads: combine nchunk partials per group -> mean, rstd
+// grid (G, B), 256 threads: combine the nchunk partials of one (b, g) -> mean, rstd
+// (strided per-thread Chan combine, then a shuffle / LDS tree)
+__device__ __forceinline__ Stat chan_shfl(Stat a, int off) {
+  Stat o{__shfl_xor(a.n, off, 64), __shfl_xor(a.m, off, 64), __shfl_xor(a.q, off, 64)};
+  return chan(a, o);
+}
 __global__ __launch_bounds__(kThreads) void gn_finalize_kernel(const float* __restrict__ part,
                                                                int nchunk, int G, float eps,
                                                                float* __restrict__ mean,
                                                                float* __restrict__ rstd) {
-  __shared__ Stat sh[kThreads];
-  const int b = blockIdx.x;
-  const int per_g = kThreads / G;  // threads per group (G <= 256)
-  const int g = threadIdx.x / per_g, lane = threadIdx.x % per_g;
+  __shared__ Stat sh[kThreads / 64];
+  const int g = blockIdx.x, b = blockIdx.y;
   Stat a{0.f, 0.f, 0.f};
-  if (g < G) {
-    for (int k = lane; k < nchunk; k += per_g) {
-      const float* p = part + (((int64_t)b * nchunk + k) * G + g) * 3;
-      a = chan(a, Stat{p[0], p[1], p[2]});
-    }
+  for (int k = threadIdx.x; k < nchunk; k += kThreads) {
+    const float* p = part + (((int64_t)b * nchunk + k) * G + g) * 3;
+    a = chan(a, Stat{p[0], p[1], p[2]});
   }
-  sh[threadIdx.x] = a;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) a = chan_shfl(a, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
   __syncthreads();
-  if (g < G && lane == 0) {
-    Stat t = sh[threadIdx.x];
-    for (int k = 1; k < per_g; ++k) t = chan(t, sh[threadIdx.x + k]);
+  if (threadIdx.x == 0) {
+    Stat t = sh[0];
+    for (int k = 1; k < kThreads / 64; ++k) t = chan(t, sh[k]);
     const float var = t.n > 0.f ? t.q / t.n : 0.f;  // biased, as torch GroupNorm
     mean[b * G + g] = t.m;
     rstd[b * G + g] = rsqrtf(var + eps);
@@ -243,47 +246,59 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
   }
 }
 
-// one WG, one thread per channel: per-sample sums, group coefficients, dgamma/dbeta
-__global__ void gn_bwd_finalize_kernel(const float* __restrict__ part, int B, int nchunk, int C,
-                                       int G, int64_t S, const float* __restrict__ gamma,
+// grid (ceil(C/64), B), 1024 threads = 64 channels x 16 chunk lanes: per-(b, c) sums of
+// the chunk partials -> sums[b][c][2] (coalesced 512-B rows, 16-way parallel over chunks)
+__global__ __launch_bounds__(1024) void gn_bwd_sum_kernel(const float* __restrict__ part,
+                                                          int nchunk, int C,
+                                                          float* __restrict__ sums) {
+  __shared__ float2 sh[16][64];
+  const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
+  float2 a = make_float2(0.f, 0.f);
+  if (c < C) {
+    for (int k = kl; k < nchunk; k += 16) {
+      const float2 v = *reinterpret_cast<const float2*>(part + (((int64_t)b * nchunk + k) * C + c) * 2);
+      a.x += v.x;
+      a.y += v.y;
+    }
+  }
+  sh[kl][cl] = a;
+  __syncthreads();
+  if (kl == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) {
+      a.x += sh[k][cl].x;
+      a.y += sh[k][cl].y;
+    }
+    *reinterpret_cast<float2*>(sums + ((int64_t)b * C + c) * 2) = a;
+  }
+}
+
+// one WG: group coefficients per (b, g) and dgamma/dbeta per channel from sums[b][c][2]
+__global__ void gn_bwd_finalize_kernel(const float* __restrict__ sums, int B, int C, int G,
+                                       int64_t S, const float* __restrict__ gamma,
                                        float* __restrict__ coef, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sA = reinterpret_cast<float*>(smem);  // [C] gamma * A
-  float* sB = sA + C;                          // [C] gamma * B
   const int cpg = C / G;
   const float inv_n = 1.f / ((float)cpg * (float)S);
-  float dg[4] = {0, 0, 0, 0}, db[4] = {0, 0, 0, 0};  // up to 4 channels per thread
-  for (int b = 0; b < B; ++b) {
-    int slot = 0;
-    for (int c = threadIdx.x; c < C; c += blockDim.x, ++slot) {
-      float a = 0.f, s = 0.f;
-      for (int k = 0; k < nchunk; ++k) {
-        const float* p = part + (((int64_t)b * nchunk + k) * C + c) * 2;
-        a += p[0];
-        s += p[1];
-      }
-      db[slot] += a;
-      dg[slot] += s;
-      sA[c] = gamma[c] * a;
-      sB[c] = gamma[c] * s;
+  for (int bg = threadIdx.x; bg < B * G; bg += blockDim.x) {
+    const int b = bg / G, g = bg % G;
+    float a = 0.f, s = 0.f;
+    for (int k = 0; k < cpg; ++k) {
+      const int c = g * cpg + k;
+      a += gamma[c] * sums[((int64_t)b * C + c) * 2];
+      s += gamma[c] * sums[((int64_t)b * C + c) * 2 + 1];
     }
-    __syncthreads();
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-      float a = 0.f, s = 0.f;
-      for (int k = 0; k < cpg; ++k) {
-        a += sA[g * cpg + k];
-        s += sB[g * cpg + k];
-      }
-      coef[(b * G + g) * 2 + 0] = a * inv_n;
-      coef[(b * G + g) * 2 + 1] = s * inv_n;
-    }
-    __syncthreads();
+    coef[bg * 2 + 0] = a * inv_n;
+    coef[bg * 2 + 1] = s * inv_n;
   }
-  int slot = 0;
-  for (int c = threadIdx.x; c < C; c += blockDim.x, ++slot) {
-    dgamma[c] = dg[slot];
-    dbeta[c] = db[slot];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, s = 0.f;
+    for (int b = 0; b < B; ++b) {
+      a += sums[((int64_t)b * C + c) * 2];
+      s += sums[((int64_t)b * C + c) * 2 + 1];
+    }
+    dbeta[c] = a;
+    dgamma[c] = s;
   }
 }
 
@@ -346,7 +361,8 @@ size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G) {
   if (B <= 0 || S <= 0 || C <= 0 || G <= 0 || C % kVec) return 0;
   GNPlan p = gn_plan(B, S, C);
   size_t fwd = (size_t)B * p.nchunk * G * 3 * sizeof(float);
-  size_t bwd = ((size_t)B * p.nchunk * C * 2 + (size_t)B * G * 2) * sizeof(float);
+  size_t bwd = ((size_t)B * p.nchunk * C * 2 + (size_t)B * G * 2 + (size_t)B * C * 2) *
+               sizeof(float);
   return (fwd > bwd ? fwd : bwd) + 256;
 }
 
@@ -367,7 +383,7 @@ int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, 
   return VD_DISPATCH_DTYPE(dtype, T, {
     gn_stats_kernel<T><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
         (const T*)x, S, C, G, p.chunk_px, p.rows_per_iter, part);
-    gn_finalize_kernel<<<B, kThreads, 0, st>>>(part, p.nchunk, G, eps, mean, rstd);
+    gn_finalize_kernel<<<dim3(G, B), kThreads, 0, st>>>(part, p.nchunk, G, eps, mean, rstd);
     const int grid = apply_grid((int64_t)B * S * (C / kVec));
     if (silu)
       gn_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
@@ -391,6 +407,7 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
   GNPlan p = gn_plan(B, S, C);
   float* part = reinterpret_cast<float*>(workspace);
   float* coef = part + (size_t)B * p.nchunk * C * 2;
+  float* sums = coef + (size_t)B * G * 2;
   hipStream_t st = VD_STREAM(stream);
   const size_t lds = (size_t)p.rows_per_iter * C * sizeof(float2);
   const int grid = apply_grid((int64_t)B * S * (C / kVec));
@@ -403,9 +420,9 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
       gn_bwd_reduce_kernel<T, false><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
           p.rows_per_iter, part, drop);
-    gn_bwd_finalize_kernel<<<1, kThreads, 2 * C * sizeof(float), st>>>(part, B, p.nchunk, C, G,
-                                                                       S, gamma, coef, dgamma,
-                                                                       dbeta);
+    gn_bwd_sum_kernel<<<dim3((unsigned)vd_cdiv(C, 64), B), 1024, 0, st>>>(part, p.nchunk, C,
+                                                                          sums);
+    gn_bwd_finalize_kernel<<<1, kThreads, 0, st>>>(sums, B, C, G, S, gamma, coef, dgamma, dbeta);
     if (silu)
       gn_bwd_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, (const T*)dy, gamma,
                                                               beta, mean, rstd, coef, (T*)dx, B,
