@@ -29,6 +29,7 @@
 // v_mfma_f32_32x32x2_f32 with the same structure (exact fp32 products).
 #include "vd_common.h"
 #include <math.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -141,6 +142,7 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) { return pack2bf
 template <typename T> struct XOp;
 template <> struct XOp<bf16_t> {
   bf16x8 b[2];
+  XOp() = default;
   __device__ __forceinline__ explicit XOp(const f32x16& X) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -154,6 +156,7 @@ template <> struct XOp<bf16_t> {
 };
 template <> struct XOp<float> {
   f32x16 x;
+  XOp() = default;
   __device__ __forceinline__ explicit XOp(const f32x16& X) : x(X) {}
 };
 
@@ -184,6 +187,64 @@ __device__ __forceinline__ void mma_tr(f32x16& acc, const T* tile, int sum0, int
     for (int r = 0; r < 16; ++r) {
       const float a = tile[toff<T, D>(sum0 + (r & 3) + 8 * (r >> 2) + 4 * hh, c)];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, X.x[r], acc, 0, 0, 0);
+    }
+  }
+}
+
+// NB-block forms: one LDS fragment read feeds NB MFMAs (NB 32-row blocks per wave), which
+// halves the LDS bytes per FLOP at NB = 2 -- the fragment reads, not the MFMAs, bound the
+// single-block kernels.
+template <typename T, int D, int NB>
+__device__ __forceinline__ void mma_rows_nb(f32x16 (&acc)[NB], const T* tile, int row0,
+                                            const RowFrag<T, D> (&b)[NB], int lane) {
+  const int r = row0 + (lane & 31), hh = lane >> 5;
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + toff<T, D>(r, 16 * s + 8 * hh));
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[j].f[s], acc[j], 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < D / 2; ++s) {
+      const float a = tile[toff<T, D>(r, 2 * s + hh)];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[j].f[s], acc[j], 0, 0, 0);
+    }
+  }
+}
+
+template <typename T, int D, int NB>
+__device__ __forceinline__ void mma_tr_nb(f32x16 (&acc)[NB], const T* tile, int sum0, int col0,
+                                          const XOp<T> (&X)[NB], int lane) {
+  const int hh = lane >> 5;
+  if constexpr (sizeof(T) == 2) {
+    const int g = lane >> 4, fr = lane & 15;
+    const int q4 = fr >> 2, p4 = fr & 3;
+    const int col = col0 + 16 * (g & 1) + 4 * p4;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int kr = sum0 + 16 * s2 + 4 * (g >> 1) + q4;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_bf16x4*)(tile + toff<T, D>(kr, col)));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_bf16x4*)(tile + toff<T, D>(kr + 8, col)));
+      const bf16x8 aop = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aop, X[j].b[s2], acc[j], 0, 0, 0);
+    }
+  } else {
+    const int c = col0 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float a = tile[toff<T, D>(sum0 + (r & 3) + 8 * (r >> 2) + 4 * hh, c)];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, X[j].x[r], acc[j], 0, 0, 0);
     }
   }
 }
@@ -378,82 +439,104 @@ size_t tile_loop_lds() {
 }
 
 // ================================================================== forward
-template <typename T, int D>
+// WG = 4 waves x NB x 32 queries.
+template <typename T, int D, int NB>
 __global__ __launch_bounds__(kThreads, 1) void attn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   const int seq = blockIdx.y;
-  const int q0 = blockIdx.x * kRows + wave * 32;
+  const int q0 = blockIdx.x * (kRows * NB) + wave * 32 * NB;
   const int64_t base = qa(seq);
-  const int myq = q0 + (lane & 31);
 
-  RowFrag<T, D> qf;
-  qf.load(q + base, ts, myq, n, lane);
-  f32x16 oacc[D / 32];
+  RowFrag<T, D> qf[NB];
 #pragma unroll
-  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
-  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < NB; ++j) qf[j].load(q + base, ts, q0 + 32 * j + (lane & 31), n, lane);
+  f32x16 oacc[D / 32][NB];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) oacc[i][j] = f32x16{};
+  float m[NB], l[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
   const float c = scale * kLog2e;
 
   tile_loop<T, D, false>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
                          [&](int t, const T* Kt, const T* Vt, const float*) {
     const int key0 = t * kTile;
-    f32x16 s[2];
+    f32x16 s[2][NB];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      s[h] = f32x16{};
-      mma_rows<T, D>(s[h], Kt, 32 * h, qf, lane);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) s[h][j] = f32x16{};
+      mma_rows_nb<T, D, NB>(s[h], Kt, 32 * h, qf, lane);
     }
-    // online softmax in the log2 domain; keys on registers, query on the lane.
     // Only the tail tile needs the key mask (wave-uniform branch).
     if (key0 + kTile > n) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (key0 + 32 * h + acc_row(r, hh) >= n) s[h][r] = -INFINITY;
+          if (key0 + 32 * h + acc_row(r, hh) >= n)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) s[h][j][r] = -INFINITY;
     }
-    float tmax = s[0][0];
+    XOp<T> p[2][NB];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int j = 0; j < NB; ++j) {
+      // online softmax in the log2 domain; keys on registers, query on the lane
+      float tmax = s[0][j][0];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[h][r]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;  // c > 0: max commutes with the scale
-    // exact lazy rescale: only when some row max of this wave grew
-    if (!__all(tmax <= m)) {
-      const float mnew = fmaxf(m, tmax);
-      const float alpha = fast_exp2(m - mnew);
-      m = mnew;
-      l *= alpha;
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int i = 0; i < D / 32; ++i)
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[h][j][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;  // c > 0: max commutes with scale
+      // exact lazy rescale: only when some row max of this block grew
+      if (!__all(tmax <= m[j])) {
+        const float mnew = fmaxf(m[j], tmax);
+        const float alpha = fast_exp2(m[j] - mnew);
+        m[j] = mnew;
+        l[j] *= alpha;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
-    }
-    const float nm = -m;
-    float psum = 0.f;
+        for (int i = 0; i < D / 32; ++i)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fast_exp2(fmaf(s[h][r], c, nm));
-        s[h][r] = p;
-        psum += p;
+          for (int r = 0; r < 16; ++r) oacc[i][j][r] *= alpha;
       }
-    l += psum;
-    const XOp<T> p0(s[0]), p1(s[1]);
+      const float nm = -m[j];
+      float psum = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(fmaf(s[h][j][r], c, nm));
+          s[h][j][r] = pv;
+          psum += pv;
+        }
+      l[j] += psum;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) p[h][j] = XOp<T>(s[h][j]);
+    }
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {
-      mma_tr<T, D>(oacc[i], Vt, 0, 32 * i, p0, lane);
-      mma_tr<T, D>(oacc[i], Vt, 32, 32 * i, p1, lane);
+      mma_tr_nb<T, D, NB>(oacc[i], Vt, 0, 32 * i, p[0], lane);
+      mma_tr_nb<T, D, NB>(oacc[i], Vt, 32, 32 * i, p[1], lane);
     }
   });
-  l += __shfl_xor(l, 32, 64);
-  const float inv = 1.f / l;
-  store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, oacc, inv, lane);
-  if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m + log2f(l)) / kLog2e;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int myq = q0 + 32 * j + (lane & 31);
+    const float lt = l[j] + __shfl_xor(l[j], 32, 64);
+    f32x16 out[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) out[i] = oacc[i][j];
+    store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, out, 1.f / lt, lane);
+    if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m[j] + log2f(lt)) / kLog2e;
+  }
 }
 
 // ================================================================== delta = rowsum(dO * O)
@@ -480,7 +563,7 @@ __global__ void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__
 }
 
 // ================================================================== backward: dQ
-template <typename T, int D>
+template <typename T, int D, int NB>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
     const T* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -488,46 +571,64 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int seq = blockIdx.y;
-  const int q0 = blockIdx.x * kRows + wave * 32;
+  const int q0 = blockIdx.x * (kRows * NB) + wave * 32 * NB;
   const int64_t base = qa(seq);
-  const int myq = q0 + (lane & 31);
   const float c = scale * kLog2e;
 
-  RowFrag<T, D> qf, of;
-  qf.load(q + base, ts, myq, n, lane);
-  of.load(dout + oa(seq), ots, myq, n, lane);
-  const float nlse2 = myq < n ? -lse[(int64_t)seq * n + myq] * kLog2e : 0.f;
-  const float dlt = myq < n ? delta[(int64_t)seq * n + myq] : 0.f;
-  f32x16 acc[D / 32];
+  RowFrag<T, D> qf[NB], of[NB];
+  float nlse2[NB], dlt[NB];
 #pragma unroll
-  for (int i = 0; i < D / 32; ++i) acc[i] = f32x16{};
+  for (int j = 0; j < NB; ++j) {
+    const int myq = q0 + 32 * j + (lane & 31);
+    qf[j].load(q + base, ts, myq, n, lane);
+    of[j].load(dout + oa(seq), ots, myq, n, lane);
+    nlse2[j] = myq < n ? -lse[(int64_t)seq * n + myq] * kLog2e : 0.f;
+    dlt[j] = myq < n ? delta[(int64_t)seq * n + myq] : 0.f;
+  }
+  f32x16 acc[D / 32][NB];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
 
   tile_loop<T, D, false>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
                          [&](int, const T* Kt, const T* Vt, const float*) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      f32x16 s = f32x16{}, dp = f32x16{};
-      mma_rows<T, D>(s, Kt, 32 * h, qf, lane);
-      mma_rows<T, D>(dp, Vt, 32 * h, of, lane);
+      f32x16 s[NB], dp[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) s[j] = dp[j] = f32x16{};
+      mma_rows_nb<T, D, NB>(s, Kt, 32 * h, qf, lane);
+      mma_rows_nb<T, D, NB>(dp, Vt, 32 * h, of, lane);
       // keys past n have zero K/V rows: their dS^T multiplies a zero K row in the
       // dQ product, so no mask is needed here
+      XOp<T> ds[NB];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fast_exp2(fmaf(s[r], c, nlse2));
-        s[r] = p * (dp[r] - dlt);  // dS^T
+      for (int j = 0; j < NB; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(fmaf(s[j][r], c, nlse2[j]));
+          s[j][r] = pv * (dp[j][r] - dlt[j]);  // dS^T
+        }
+        ds[j] = XOp<T>(s[j]);
       }
-      const XOp<T> ds(s);
 #pragma unroll
-      for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(acc[i], Kt, 32 * h, 32 * i, ds, lane);
+      for (int i = 0; i < D / 32; ++i) mma_tr_nb<T, D, NB>(acc[i], Kt, 32 * h, 32 * i, ds, lane);
     }
   });
-  store_transposed<T, D / 32>(dq + base, ts, myq, n, 0, acc, scale, lane);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    f32x16 out[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) out[i] = acc[i][j];
+    store_transposed<T, D / 32>(dq + base, ts, q0 + 32 * j + (lane & 31), n, 0, out, scale, lane);
+  }
 }
 
 // ================================================================== backward: dK, dV
-// grid.z splits the OUTPUT columns of dK/dV in DO-wide slices (register budget
-// at D = 256); S and dP always contract over the full D.
-template <typename T, int D, int DO>
+// WG = 4 waves x NB x 32 keys.  grid.z splits the OUTPUT columns of dK/dV in DO-wide
+// slices (register budget at D = 256); S and dP always contract over the full D.
+template <typename T, int D, int DO, int NB>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
     const T* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -537,17 +638,21 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   const int seq = blockIdx.y;
   const int d0 = blockIdx.z * DO;
-  const int k0 = blockIdx.x * kRows + wave * 32;
+  const int k0 = blockIdx.x * (kRows * NB) + wave * 32 * NB;
   const int64_t base = qa(seq), obase = oa(seq);
-  const int mykey = k0 + (lane & 31);
   const float c = scale * kLog2e;
 
-  RowFrag<T, D> kf, vf;
-  kf.load(k + base, ts, mykey, n, lane);
-  vf.load(v + base, ts, mykey, n, lane);
-  f32x16 adv[DO / 32], adk[DO / 32];
+  RowFrag<T, D> kf[NB], vf[NB];
 #pragma unroll
-  for (int i = 0; i < DO / 32; ++i) adv[i] = adk[i] = f32x16{};
+  for (int j = 0; j < NB; ++j) {
+    kf[j].load(k + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+    vf[j].load(v + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+  }
+  f32x16 adv[DO / 32][NB], adk[DO / 32][NB];
+#pragma unroll
+  for (int i = 0; i < DO / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) adv[i][j] = adk[i][j] = f32x16{};
 
   // query rows past n have zero Q / dO rows and zero lse / delta, so they add nothing
   // to dV (dO = 0) or dK (dS = p * (0 - 0)): no mask needed.
@@ -556,33 +661,53 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
                         [&](int, const T* Qt, const T* Ot, const float* L) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      f32x16 s = f32x16{}, dp = f32x16{};
-      mma_rows<T, D>(s, Qt, 32 * h, kf, lane);   // S[q][key]
-      mma_rows<T, D>(dp, Ot, 32 * h, vf, lane);  // dP[q][key]
+      f32x16 s[NB], dp[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) s[j] = dp[j] = f32x16{};
+      mma_rows_nb<T, D, NB>(s, Qt, 32 * h, kf, lane);   // S[q][key]
+      mma_rows_nb<T, D, NB>(dp, Ot, 32 * h, vf, lane);  // dP[q][key]
       // registers 4g..4g+3 are rows 8g + 4hh + 0..3: one b128 read per constant
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 ls = *reinterpret_cast<const float4*>(L + 32 * h + 8 * g + 4 * hh);
         const float4 dl = *reinterpret_cast<const float4*>(L + 64 + 32 * h + 8 * g + 4 * hh);
-        const float lv[4] = {ls.x, ls.y, ls.z, ls.w}, dlv[4] = {dl.x, dl.y, dl.z, dl.w};
+        const float lv[4] = {-ls.x * kLog2e, -ls.y * kLog2e, -ls.z * kLog2e, -ls.w * kLog2e};
+        const float dlv[4] = {dl.x, dl.y, dl.z, dl.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e;
-          const float p = fast_exp2(fmaf(s[r], c, -lv[e] * kLog2e));
-          s[r] = p;
-          dp[r] = p * (dp[r] - dlv[e]);  // dS
-        }
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const float pv = fast_exp2(fmaf(s[j][r], c, lv[e]));
+            s[j][r] = pv;
+            dp[j][r] = pv * (dp[j][r] - dlv[e]);  // dS
+          }
       }
-      const XOp<T> pp(s), ds(dp);
+      XOp<T> pp[NB], ds[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        pp[j] = XOp<T>(s[j]);
+        ds[j] = XOp<T>(dp[j]);
+      }
 #pragma unroll
       for (int i = 0; i < DO / 32; ++i) {
-        mma_tr<T, D>(adv[i], Ot, 32 * h, d0 + 32 * i, pp, lane);  // dV^T += dO^T P
-        mma_tr<T, D>(adk[i], Qt, 32 * h, d0 + 32 * i, ds, lane);  // dK^T += Q^T dS
+        mma_tr_nb<T, D, NB>(adv[i], Ot, 32 * h, d0 + 32 * i, pp, lane);  // dV^T += dO^T P
+        mma_tr_nb<T, D, NB>(adk[i], Qt, 32 * h, d0 + 32 * i, ds, lane);  // dK^T += Q^T dS
       }
     }
   });
-  store_transposed<T, DO / 32>(dk + base, ts, mykey, n, d0, adk, scale, lane);
-  store_transposed<T, DO / 32>(dv + base, ts, mykey, n, d0, adv, 1.f, lane);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int mykey = k0 + 32 * j + (lane & 31);
+    f32x16 ok[DO / 32], ov[DO / 32];
+#pragma unroll
+    for (int i = 0; i < DO / 32; ++i) {
+      ok[i] = adk[i][j];
+      ov[i] = adv[i][j];
+    }
+    store_transposed<T, DO / 32>(dk + base, ts, mykey, n, d0, ok, scale, lane);
+    store_transposed<T, DO / 32>(dv + base, ts, mykey, n, d0, ov, 1.f, lane);
+  }
 }
 
 // ------------------------------------------------------------------ launchers
@@ -599,14 +724,29 @@ int check_attn(const vd_attn_desc* d) {
   return VD_OK;
 }
 
-template <typename T, int D>
-int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
-             float* lse, hipStream_t st) {
+// rows per wave (NB x 32): 2 for bf16 up to D = 128 (LDS fragment reuse), 1 otherwise.
+// VDIFF_ATTN_NB=1|2 overrides for A/B measurements.
+int pick_nb(int D, bool bf16, int kind) {
+  static const int env = [] {
+    const char* e = getenv("VDIFF_ATTN_NB");
+    return e ? atoi(e) : 0;
+  }();
+  if (env == 1 || env == 2) return (D == 256 || !bf16) ? 1 : env;
+  if (!bf16 || D == 256) return 1;
+  // dK/dV: NB = 2 spills into the unified register file (256 VGPRs) and measured slower
+  // (D = 64: 38.3 ms vs 34.7 ms at N = 262144); fwd / dQ gain 14% / 12%.
+  if (kind == 2) return 1;
+  return 2;
+}
+
+template <typename T, int D, int NB>
+int fwd_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
+               float* lse, hipStream_t st) {
   const size_t lds = tile_loop_lds<T, D, false>();
-  auto kern = attn_fwd_kernel<T, D>;
+  auto kern = attn_fwd_kernel<T, D, NB>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows * NB), (unsigned)d->nseq);
   kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
                                     d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
                                     d->token_stride,
@@ -616,9 +756,31 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
 }
 
 template <typename T, int D>
+int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
+             float* lse, hipStream_t st) {
+  if (pick_nb(D, kDMA<T>, 0) == 2) return fwd_launch<T, D, (kDMA<T> && D != 256) ? 2 : 1>(d, q, k, v, o, lse, st);
+  return fwd_launch<T, D, 1>(d, q, k, v, o, lse, st);
+}
+
+template <typename T, int D, int NB>
+int dq_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+              const void* dout, const float* lse, const float* delta, void* dq, hipStream_t st) {
+  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+  const size_t lds = tile_loop_lds<T, D, false>();
+  auto kern = attn_bwd_dq_kernel<T, D, NB>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows * NB), (unsigned)d->nseq);
+  kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
+                                    delta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
+                                    d->o_token_stride, d->scale);
+  return vd::check_launch("attn_bwd_dq");
+}
+
+template <typename T, int D>
 int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, const void* o,
                 const void* dout, const float* lse, void* dq, void* ws, hipStream_t st) {
-  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   float* delta = reinterpret_cast<float*>(ws);
   const int64_t rows = (int64_t)d->nseq * d->seq_len;
@@ -628,34 +790,38 @@ int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void*
                                               d->seq_len, oa, d->o_token_stride);
   int rc = vd::check_launch("attn_delta");
   if (rc) return rc;
-  const size_t lds = tile_loop_lds<T, D, false>();
-  auto kern = attn_bwd_dq_kernel<T, D>;
+  if (pick_nb(D, kDMA<T>, 1) == 2)
+    return dq_launch<T, D, (kDMA<T> && D != 256) ? 2 : 1>(d, q, k, v, dout, lse, delta, dq, st);
+  return dq_launch<T, D, 1>(d, q, k, v, dout, lse, delta, dq, st);
+}
+
+template <typename T, int D, int NB>
+int dkdv_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                const void* dout, const float* lse, const float* delta, void* dk, void* dv,
+                hipStream_t st) {
+  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+  constexpr int DO = D > 128 ? 128 : D;
+  const size_t lds = tile_loop_lds<T, D, true>();
+  auto kern = attn_bwd_dkdv_kernel<T, D, DO, NB>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows * NB), (unsigned)d->nseq, D / DO);
   kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
-                                    delta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
+                                    delta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
                                     d->o_token_stride, d->scale);
-  return vd::check_launch("attn_bwd_dq");
+  return vd::check_launch("attn_bwd_dkdv");
 }
 
 template <typename T, int D>
 int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                   const void* dout, const float* lse, void* dk, void* dv, void* ws,
                   hipStream_t st) {
-  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
-  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const float* delta = reinterpret_cast<const float*>(ws);
-  constexpr int DO = D > 128 ? 128 : D;
-  const size_t lds = tile_loop_lds<T, D, true>();
-  auto kern = attn_bwd_dkdv_kernel<T, D, DO>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows), (unsigned)d->nseq, D / DO);
-  kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
-                                    delta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
-                                    d->o_token_stride, d->scale);
-  return vd::check_launch("attn_bwd_dkdv");
+  // (NB = 2 at D = 128 needs > 512 registers; hipcc 7.2 also crashes on it)
+  if (pick_nb(D, kDMA<T>, 2) == 2)
+    return dkdv_launch<T, D, (kDMA<T> && D <= 64) ? 2 : 1>(d, q, k, v, dout, lse, delta, dk, dv, st);
+  return dkdv_launch<T, D, 1>(d, q, k, v, dout, lse, delta, dk, dv, st);
 }
 
 #define VD_DISPATCH_HEAD(D_, FN, ...)                        \

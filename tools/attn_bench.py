@@ -51,7 +51,25 @@ def bench(C, N, reps, bwd=True):
               f"({f / avg / 1e9 / 2500 * 100:5.1f}% of 2.5 PF)", flush=True)
 
 
+CALIB_ELEMS = 1 << 27   # bf16 elements per operand: 256 MiB each, past the 256 MiB L3
+
+
+def calib():
+    """PMC calibration launch: q_sample over bf16 streams (16 B per lane loads and stores).
+    Algorithmic bytes per launch: 2 reads + 1 write of CALIB_ELEMS bf16 (tools/pmc_traffic.py)."""
+    x = torch.randn(CALIB_ELEMS, device="cuda", dtype=torch.bfloat16).view(4, -1)
+    e = torch.randn_like(x)
+    t = torch.tensor([1, 2, 3, 4], device="cuda")
+    tab = torch.linspace(0.1, 0.9, 1000, device="cuda")
+    for _ in range(3):
+        ops.q_sample(x, e, t, tab, tab)
+    torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
+    if "--calib" in sys.argv:
+        calib()
+        sys.argv.remove("--calib")
     check()
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     for C, N in ((64, 262144), (128, 65536), (256, 16384)):
