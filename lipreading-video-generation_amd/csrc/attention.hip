@@ -30,22 +30,30 @@
 #include "vd_common.h"
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 namespace {
 
-constexpr int kThreads = 256;  // 4 waves
-constexpr int kRows = 128;     // queries (fwd, dQ) or keys (dKdV) per workgroup
+// A workgroup is NW waves (4 or 8); each wave owns NB x 32 rows (queries for fwd / dQ,
+// keys for dK/dV), so a workgroup covers 32 * NB * NW rows and shares every LDS tile
+// among its NW waves.
 constexpr int kTile = 64;      // keys (fwd, dQ) or queries (dKdV) per LDS tile
 constexpr float kLog2e = 1.4426950408889634f;
 
 // ------------------------------------------------------------------ LDS tiles
-// bf16 tile [64][D]: 16-B chunks XOR-swizzled per row so the 32-row fragment
-// reads (ds_read_b128) hit distinct bank slots.  fp32 tile: rows of D+1 floats.
+// bf16 tile [64][D]: 16-B chunks XOR-swizzled per row.  Two read shapes must both be
+// conflict-free (bank = byte/4 mod 64, MI355X_MICROARCH.md "LDS"):
+//  * ds_read_b128 row fragments: a 16-lane group reads one chunk of 16 rows
+//    {0-3,12-15,20-27} or {4-11,16-19,28-31} (+32) -> those rows need distinct slots;
+//  * ds_read_b64_tr_b16: a 32-lane group reads 4 consecutive chunks of rows 4m..4m+3
+//    -> the four 64-B pieces must fall in different quarters of the 256-B bank line.
+// D = 64 (two rows per bank line): bit 2 of the XOR alternates between rows 4m and 4m+2;
+// D >= 128: bits 2-3 of the XOR are r & 3.  fp32 tile: rows of D+1 floats.
 template <int D>
 __device__ __forceinline__ int swz_row(int r) {
   if constexpr (D == 32) return (0x1320 >> (4 * ((r >> 2) & 3))) & 3;
-  else if constexpr (D == 64) return (r >> 1) & 7;
-  else return r & 15;
+  else if constexpr (D == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  else return ((r & 3) << 2) | ((r >> 2) & 3);
 }
 template <typename T, int D>
 __device__ __forceinline__ int toff(int r, int c) {
@@ -56,16 +64,16 @@ template <typename T, int D>
 constexpr int tile_elems() { return sizeof(T) == 2 ? kTile * D : kTile * (D + 1); }
 
 // global rows [tok0, tok0+64) x [0, D) -> LDS tile (zero rows beyond n)
-template <typename T, int D>
+template <typename T, int D, int NW>
 struct Stager {
   static constexpr int EPC = 16 / sizeof(T);
   static constexpr int CPR = D / EPC;
-  static constexpr int NCH = kTile * CPR / kThreads;
+  static constexpr int NCH = kTile * CPR / (64 * NW);
   uint4 r[NCH > 0 ? NCH : 1];
   __device__ __forceinline__ void load(const T* base, int64_t ts, int tok0, int n, int tid) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int q = tid + i * kThreads;
+      const int q = tid + i * 64 * NW;
       const int row = q / CPR, cc = q % CPR;
       const int tok = tok0 + row;
       r[i] = tok < n ? *reinterpret_cast<const uint4*>(base + (int64_t)tok * ts + cc * EPC)
@@ -75,7 +83,7 @@ struct Stager {
   __device__ __forceinline__ void store(T* tile, int tid) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int q = tid + i * kThreads;
+      const int q = tid + i * 64 * NW;
       const int row = q / CPR, cc = q % CPR;
       if constexpr (sizeof(T) == 2) {
         *reinterpret_cast<uint4*>(tile + toff<T, D>(row, cc * EPC)) = r[i];
@@ -104,6 +112,20 @@ template <int D> struct RowFrag<bf16_t, D> {
       f[s] = __builtin_bit_cast(bf16x8, v);
     }
   }
+  // pre-multiply by the softmax scale (x log2 e): the MFMA then emits S in log2 units, so
+  // no per-element scaling is left in the softmax (one extra bf16 rounding of the operand)
+  __device__ __forceinline__ void scale(float c) {
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const uint4 w = __builtin_bit_cast(uint4, f[s]);
+      const uint32_t in[4] = {w.x, w.y, w.z, w.w};
+      uint32_t out[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        out[e] = pack2bf(__uint_as_float(in[e] << 16) * c, __uint_as_float(in[e] & 0xffff0000u) * c);
+      f[s] = __builtin_bit_cast(bf16x8, make_uint4(out[0], out[1], out[2], out[3]));
+    }
+  }
 };
 template <int D> struct RowFrag<float, D> {
   float f[D / 2];
@@ -111,6 +133,10 @@ template <int D> struct RowFrag<float, D> {
     const int hh = lane >> 5;
 #pragma unroll
     for (int s = 0; s < D / 2; ++s) f[s] = tok < n ? base[(int64_t)tok * ts + 2 * s + hh] : 0.f;
+  }
+  __device__ __forceinline__ void scale(float c) {
+#pragma unroll
+    for (int s = 0; s < D / 2; ++s) f[s] *= c;
   }
 };
 
@@ -298,20 +324,41 @@ typedef __attribute__((address_space(3))) void lds_void;
 template <typename T> constexpr bool kDMA = sizeof(T) == 2;
 
 template <int D> constexpr int nstage() { return D <= 64 ? 4 : (D == 128 ? 3 : 2); }
-template <int D> constexpr int dma_ipw() { return kTile * D * 2 / 1024 / 4; }  // per wave per tile
+// DMA instructions (1 KiB each) per wave per tile
+template <int D, int NW> constexpr int dma_ipw() { return kTile * D * 2 / 1024 / NW; }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                           0x00020000);
+// Buffer resource words: base, stride 0, num_records = bytes (the range check zero-fills
+// beyond it), raw dword format.
+typedef int __attribute__((ext_vector_type(4))) rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  return rsrc_t{(int)(uint32_t)a, (int)(uint32_t)((a >> 32) & 0xffff), (int)bytes, 0x00020000};
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(const lds_void*)p;
+}
+
+// The LDS-DMA is issued from inline asm on purpose: the compiler's waitcnt pass cannot tell
+// which LDS bytes a builtin buffer_load...lds writes, so it put an s_waitcnt vmcnt(0) in
+// front of the first LDS read after it -- draining the whole ring every tile.  The ring's
+// own counted vmcnt + s_barrier (vm_wait_barrier) is what orders these writes.
+template <int BYTES>
+__device__ __forceinline__ void dma_lds(rsrc_t rs, uint32_t lds, uint32_t voff) {
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+                 ::"s"(lds), "v"(voff), "s"(rs));
+  else
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+                 ::"s"(lds), "v"(voff), "s"(rs));
 }
 
 // this wave's share of one [64 x D] bf16 tile: logical 16-B chunk c of row r lands at the
 // swizzled position toff(r, 8c) (the DMA writes lane-linearly, so the SOURCE chunk is
 // permuted by the same involution)
-template <int D>
-__device__ __forceinline__ void dma_tile(__amdgpu_buffer_rsrc_t rs, char* lds, int tok0, int n,
+template <int D, int NW>
+__device__ __forceinline__ void dma_tile(rsrc_t rs, char* lds, int tok0, int n,
                                          uint32_t ts_bytes, int wave, int lane) {
-  constexpr int CPL = D / 8, RPI = 64 / CPL, IPW = dma_ipw<D>();
+  constexpr int CPL = D / 8, RPI = 64 / CPL, IPW = dma_ipw<D, NW>();
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
     const int gi = wave * IPW + i;
@@ -319,22 +366,22 @@ __device__ __forceinline__ void dma_tile(__amdgpu_buffer_rsrc_t rs, char* lds, i
     const int c = (lane % CPL) ^ swz_row<D>(row);
     const int tok = tok0 + row;
     const uint32_t voff = tok < n ? (uint32_t)tok * ts_bytes + (uint32_t)c * 16u : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + gi * 1024), 16, voff, 0, 0, 0);
+    dma_lds<16>(rs, lds_addr(lds + gi * 1024), voff);
   }
 }
 
 // 64 fp32 row constants (one dword per lane)
-__device__ __forceinline__ void dma_rowc(__amdgpu_buffer_rsrc_t rs, char* lds, int tok0,
-                                         int lane) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 4, (uint32_t)(tok0 + lane) * 4u, 0,
-                                           0, 0);
+__device__ __forceinline__ void dma_rowc(rsrc_t rs, char* lds, int tok0, int lane) {
+  dma_lds<4>(rs, lds_addr(lds), (uint32_t)(tok0 + lane) * 4u);
 }
 
 template <int N>
 __device__ __forceinline__ void vm_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// compiler-visible (the waitcnt pass then knows every earlier global load has landed and
+// puts no waits of its own inside the ring loop); 0x0F70 = vmcnt(0), expcnt/lgkmcnt untouched
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 __device__ __forceinline__ uint32_t seq_bytes(int n, int64_t ts, int D, int esz) {
   return (uint32_t)(((int64_t)(n - 1) * ts + D) * esz);
@@ -343,7 +390,7 @@ __device__ __forceinline__ uint32_t seq_bytes(int n, int64_t ts, int D, int esz)
 // Runs body(t, tileA, tileB) over all 64-row tiles of two row streams (a, b) of one
 // sequence; with RC, the fp32 row constants rc0/rc1 of the tile are staged too and
 // passed as body's fourth argument (float* [rc0 64 | rc1 64]).
-template <typename T, int D, bool RC, typename Body>
+template <typename T, int D, bool RC, int NW, typename Body>
 __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, int64_t ts_a,
                                           int64_t ts_b, const float* rc0, const float* rc1, int n,
                                           int tid, Body&& body) {
@@ -354,10 +401,10 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
   if constexpr (kDMA<T>) {
     constexpr int NST = nstage<D>();
     constexpr int STAGE_BYTES = 2 * TE * 2 + (RC ? 768 : 0);
-    constexpr int PER_TILE = 2 * dma_ipw<D>() + (RC ? 1 : 0);
+    constexpr int PER_TILE = 2 * dma_ipw<D, NW>() + (RC ? 1 : 0);
     const auto ra = make_rsrc(a, seq_bytes(n, ts_a, D, 2));
     const auto rb = make_rsrc(b, seq_bytes(n, ts_b, D, 2));
-    __amdgpu_buffer_rsrc_t r0, r1;
+    rsrc_t r0, r1;
     if constexpr (RC) {
       r0 = make_rsrc(rc0, (uint32_t)n * 4u);
       r1 = make_rsrc(rc1, (uint32_t)n * 4u);
@@ -366,9 +413,9 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
     auto issue = [&](int t) {
       char* st = smem + (t % NST) * STAGE_BYTES;
       const int tok0 = t * kTile;
-      dma_tile<D>(ra, st, tok0, n, tsa, wave, lane);
-      dma_tile<D>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
-      if constexpr (RC) {  // waves 0/1 stage the two constants, 2/3 a throw-away copy
+      dma_tile<D, NW>(ra, st, tok0, n, tsa, wave, lane);
+      dma_tile<D, NW>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
+      if constexpr (RC) {  // waves 0/1 stage the two constants, the others a throw-away copy
         // (every wave issues the same number of DMAs, so one vmcnt fits all)
         char* rcs = st + 4 * TE + (wave < 2 ? wave * 256 : 512);
         dma_rowc(wave == 1 ? r1 : r0, rcs, tok0, lane);
@@ -388,7 +435,7 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
   } else {
     T* lds = reinterpret_cast<T*>(smem);
     float* rcl = reinterpret_cast<float*>(smem + 2 * TE * sizeof(T));
-    Stager<T, D> sa, sb;
+    Stager<T, D, NW> sa, sb;
     float v0 = 0.f, v1 = 0.f;
     auto ldrc = [&](int tok0) {
       if constexpr (RC) {
@@ -440,44 +487,54 @@ size_t tile_loop_lds() {
 
 // ================================================================== forward
 // WG = 4 waves x NB x 32 queries.
-template <typename T, int D, int NB>
-__global__ __launch_bounds__(kThreads, 1) void attn_fwd_kernel(
+//
+// Softmax VALU is what bounds this kernel at D = 64 (per score: exp 8 cycles + add 4 +
+// half a cvt, against 2 x 16 MACs of MFMA), so the per-score work is cut to the minimum:
+//  * Q is pre-scaled by scale*log2(e), so S' = S * scale * log2(e) leaves the MFMA;
+//  * the S' accumulator starts at -m (a per-lane splat: the query is on the lane), so the
+//    MFMA emits S' - m and the probability is a bare v_exp_f32;
+//  * no per-tile max: m is a reference point that may lag the true running max.  While
+//    every p stays below 2^kLag the sums are exact in fp32 (O / l is invariant to m); a
+//    tile whose row sum reaches 2^kLag (or is inf, e.g. the first tile with m = -inf) is
+//    recomputed with its true max (rare path), which resets m and rescales O and l.
+constexpr float kLagSum = 65536.f;  // 2^16: p <= 2^16, l <= 2^16 * N -- far from overflow
+
+template <typename T, int D, int NB, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   const int seq = blockIdx.y;
-  const int q0 = blockIdx.x * (kRows * NB) + wave * 32 * NB;
+  const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
 
   RowFrag<T, D> qf[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) qf[j].load(q + base, ts, q0 + 32 * j + (lane & 31), n, lane);
+  for (int j = 0; j < NB; ++j) {
+    qf[j].load(q + base, ts, q0 + 32 * j + (lane & 31), n, lane);
+    qf[j].scale(scale * kLog2e);
+  }
   f32x16 oacc[D / 32][NB];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i)
 #pragma unroll
     for (int j = 0; j < NB; ++j) oacc[i][j] = f32x16{};
   float m[NB], l[NB];
+  f32x16 negm[NB];  // -m splat: the initial S' accumulator
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     m[j] = -INFINITY;
     l[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) negm[j][r] = INFINITY;
   }
-  const float c = scale * kLog2e;
 
-  tile_loop<T, D, false>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
+  tile_loop<T, D, false, NW>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
                          [&](int t, const T* Kt, const T* Vt, const float*) {
     const int key0 = t * kTile;
-    f32x16 s[2][NB];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int j = 0; j < NB; ++j) s[h][j] = f32x16{};
-      mma_rows_nb<T, D, NB>(s[h], Kt, 32 * h, qf, lane);
-    }
-    // Only the tail tile needs the key mask (wave-uniform branch).
-    if (key0 + kTile > n) {
+    const bool tail = key0 + kTile > n;  // only the last tile masks keys (wave-uniform)
+    auto mask = [&](f32x16 (&s)[2][NB]) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -485,39 +542,71 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_kernel(
           if (key0 + 32 * h + acc_row(r, hh) >= n)
 #pragma unroll
             for (int j = 0; j < NB; ++j) s[h][j][r] = -INFINITY;
+    };
+    f32x16 s[2][NB];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) s[h][j] = negm[j];
+      mma_rows_nb<T, D, NB>(s[h], Kt, 32 * h, qf, lane);
     }
-    XOp<T> p[2][NB];
+    if (tail) mask(s);
+    float psum[NB];
+    bool ok = true;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      // online softmax in the log2 domain; keys on registers, query on the lane
-      float tmax = s[0][j][0];
+      psum[j] = 0.f;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[h][j][r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;  // c > 0: max commutes with scale
-      // exact lazy rescale: only when some row max of this block grew
-      if (!__all(tmax <= m[j])) {
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(s[h][j][r]);
+          s[h][j][r] = pv;
+          psum[j] += pv;
+        }
+      ok = ok && psum[j] < kLagSum;  // false for inf / NaN too
+    }
+    if (!__all(ok)) {  // rare: recompute S' with the true max of this tile
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) s[h][j] = f32x16{};
+        mma_rows_nb<T, D, NB>(s[h], Kt, 32 * h, qf, lane);
+      }
+      if (tail) mask(s);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        float tmax = s[0][j][0];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[h][j][r]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float mnew = fmaxf(m[j], tmax);
-        const float alpha = fast_exp2(m[j] - mnew);
+        const float alpha = fast_exp2(m[j] - mnew);  // m = -inf: 0 (O and l are 0 then)
         m[j] = mnew;
         l[j] *= alpha;
 #pragma unroll
         for (int i = 0; i < D / 32; ++i)
 #pragma unroll
           for (int r = 0; r < 16; ++r) oacc[i][j][r] *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[j][r] = -mnew;
+        psum[j] = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = fast_exp2(s[h][j][r] - mnew);
+            s[h][j][r] = pv;
+            psum[j] += pv;
+          }
       }
-      const float nm = -m[j];
-      float psum = 0.f;
+    }
+    XOp<T> p[2][NB];
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = fast_exp2(fmaf(s[h][j][r], c, nm));
-          s[h][j][r] = pv;
-          psum += pv;
-        }
-      l[j] += psum;
+    for (int j = 0; j < NB; ++j) {
+      l[j] += psum[j];
 #pragma unroll
       for (int h = 0; h < 2; ++h) p[h][j] = XOp<T>(s[h][j]);
     }
@@ -539,10 +628,14 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_kernel(
   }
 }
 
-// ================================================================== delta = rowsum(dO * O)
+// ================================================================== row constants
+// Per query row, into the backward workspace: ndelta = -rowsum(dO * O) and
+// nlse2 = -lse * log2(e).  Both are the initial MFMA accumulators of the backward
+// kernels (dP - delta and S' - lse come out of the MFMA), negated once here.
 template <typename T, int D>
 __global__ void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__ dout,
-                                  float* __restrict__ delta, int nseq, int n, SeqAddr oa,
+                                  const float* __restrict__ lse, float* __restrict__ ndelta,
+                                  float* __restrict__ nlse2, int nseq, int n, SeqAddr oa,
                                   int64_t ots) {
   const int64_t rows = (int64_t)nseq * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
@@ -558,32 +651,41 @@ __global__ void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc += a[e] * b[e];
     }
-    delta[i] = acc;
+    ndelta[i] = -acc;
+    nlse2[i] = -lse[i] * kLog2e;
   }
 }
 
 // ================================================================== backward: dQ
-template <typename T, int D, int NB>
-__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
+// Q pre-scaled as in the forward; S' accumulator starts at -lse*log2(e) and dP^T at
+// -delta (per-lane splats, the query is on the lane), so P^T = exp2(acc) and
+// dS^T = P^T * acc_dP leave one exp and one multiply per score.
+template <typename T, int D, int NB, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
-    const T* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
     T* __restrict__ dq, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int seq = blockIdx.y;
-  const int q0 = blockIdx.x * (kRows * NB) + wave * 32 * NB;
+  const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
-  const float c = scale * kLog2e;
 
   RowFrag<T, D> qf[NB], of[NB];
-  float nlse2[NB], dlt[NB];
+  f32x16 il[NB], id[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int myq = q0 + 32 * j + (lane & 31);
     qf[j].load(q + base, ts, myq, n, lane);
+    qf[j].scale(scale * kLog2e);
     of[j].load(dout + oa(seq), ots, myq, n, lane);
-    nlse2[j] = myq < n ? -lse[(int64_t)seq * n + myq] * kLog2e : 0.f;
-    dlt[j] = myq < n ? delta[(int64_t)seq * n + myq] : 0.f;
+    const float a = myq < n ? nlse2[(int64_t)seq * n + myq] : 0.f;
+    const float b = myq < n ? ndelta[(int64_t)seq * n + myq] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      il[j][r] = a;
+      id[j][r] = b;
+    }
   }
   f32x16 acc[D / 32][NB];
 #pragma unroll
@@ -591,13 +693,16 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
 
-  tile_loop<T, D, false>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
+  tile_loop<T, D, false, NW>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
                          [&](int, const T* Kt, const T* Vt, const float*) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x16 s[NB], dp[NB];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) s[j] = dp[j] = f32x16{};
+      for (int j = 0; j < NB; ++j) {
+        s[j] = il[j];
+        dp[j] = id[j];
+      }
       mma_rows_nb<T, D, NB>(s, Kt, 32 * h, qf, lane);
       mma_rows_nb<T, D, NB>(dp, Vt, 32 * h, of, lane);
       // keys past n have zero K/V rows: their dS^T multiplies a zero K row in the
@@ -606,10 +711,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = fast_exp2(fmaf(s[j][r], c, nlse2[j]));
-          s[j][r] = pv * (dp[j][r] - dlt[j]);  // dS^T
-        }
+        for (int r = 0; r < 16; ++r) s[j][r] = fast_exp2(s[j][r]) * dp[j][r];  // dS^T
         ds[j] = XOp<T>(s[j]);
       }
 #pragma unroll
@@ -628,24 +730,26 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dq_kernel(
 // ================================================================== backward: dK, dV
 // WG = 4 waves x NB x 32 keys.  grid.z splits the OUTPUT columns of dK/dV in DO-wide
 // slices (register budget at D = 256); S and dP always contract over the full D.
-template <typename T, int D, int DO, int NB>
-__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
+// K pre-scaled by scale*log2(e); the tile's row constants (-lse*log2 e, -delta; the query
+// is the accumulator row here) are read from LDS straight into the initial accumulators.
+template <typename T, int D, int DO, int NB, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
-    const T* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
     T* __restrict__ dk, T* __restrict__ dv, int n, SeqAddr qa, int64_t ts, SeqAddr oa,
     int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   const int seq = blockIdx.y;
   const int d0 = blockIdx.z * DO;
-  const int k0 = blockIdx.x * (kRows * NB) + wave * 32 * NB;
+  const int k0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq), obase = oa(seq);
-  const float c = scale * kLog2e;
 
   RowFrag<T, D> kf[NB], vf[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     kf[j].load(k + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+    kf[j].scale(scale * kLog2e);
     vf[j].load(v + base, ts, k0 + 32 * j + (lane & 31), n, lane);
   }
   f32x16 adv[DO / 32][NB], adk[DO / 32][NB];
@@ -654,38 +758,39 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
     for (int j = 0; j < NB; ++j) adv[i][j] = adk[i][j] = f32x16{};
 
-  // query rows past n have zero Q / dO rows and zero lse / delta, so they add nothing
+  // query rows past n have zero Q / dO rows and zero row constants, so they add nothing
   // to dV (dO = 0) or dK (dS = p * (0 - 0)): no mask needed.
-  tile_loop<T, D, true>(smem, q + base, dout + obase, ts, ots, lse + (int64_t)seq * n,
-                        delta + (int64_t)seq * n, n, tid,
+  tile_loop<T, D, true, NW>(smem, q + base, dout + obase, ts, ots, nlse2 + (int64_t)seq * n,
+                        ndelta + (int64_t)seq * n, n, tid,
                         [&](int, const T* Qt, const T* Ot, const float* L) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      f32x16 s[NB], dp[NB];
-#pragma unroll
-      for (int j = 0; j < NB; ++j) s[j] = dp[j] = f32x16{};
-      mma_rows_nb<T, D, NB>(s, Qt, 32 * h, kf, lane);   // S[q][key]
-      mma_rows_nb<T, D, NB>(dp, Ot, 32 * h, vf, lane);  // dP[q][key]
       // registers 4g..4g+3 are rows 8g + 4hh + 0..3: one b128 read per constant
+      f32x16 il, id;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 ls = *reinterpret_cast<const float4*>(L + 32 * h + 8 * g + 4 * hh);
         const float4 dl = *reinterpret_cast<const float4*>(L + 64 + 32 * h + 8 * g + 4 * hh);
-        const float lv[4] = {-ls.x * kLog2e, -ls.y * kLog2e, -ls.z * kLog2e, -ls.w * kLog2e};
-        const float dlv[4] = {dl.x, dl.y, dl.z, dl.w};
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            const float pv = fast_exp2(fmaf(s[j][r], c, lv[e]));
-            s[j][r] = pv;
-            dp[j][r] = pv * (dp[j][r] - dlv[e]);  // dS
-          }
+        il[4 * g + 0] = ls.x; il[4 * g + 1] = ls.y; il[4 * g + 2] = ls.z; il[4 * g + 3] = ls.w;
+        id[4 * g + 0] = dl.x; id[4 * g + 1] = dl.y; id[4 * g + 2] = dl.z; id[4 * g + 3] = dl.w;
       }
+      f32x16 s[NB], dp[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        s[j] = il;
+        dp[j] = id;
+      }
+      mma_rows_nb<T, D, NB>(s, Qt, 32 * h, kf, lane);   // S'[q][key] - lse'
+      mma_rows_nb<T, D, NB>(dp, Ot, 32 * h, vf, lane);  // dP[q][key] - delta
       XOp<T> pp[NB], ds[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(s[j][r]);
+          s[j][r] = pv;
+          dp[j][r] *= pv;  // dS
+        }
         pp[j] = XOp<T>(s[j]);
         ds[j] = XOp<T>(dp[j]);
       }
@@ -724,57 +829,75 @@ int check_attn(const vd_attn_desc* d) {
   return VD_OK;
 }
 
-// rows per wave (NB x 32): 2 for bf16 up to D = 128 (LDS fragment reuse), 1 otherwise.
-// VDIFF_ATTN_NB=1|2 overrides for A/B measurements.
-int pick_nb(int D, bool bf16, int kind) {
+// Work shape per kernel: NB x 32 rows per wave, NW waves per workgroup.
+//   kNB2 : NB 2, NW 4 -- each LDS fragment feeds two MFMAs (bf16, D <= 128)
+//   kW8  : NB 1, NW 8 -- two waves per SIMD from one workgroup, each LDS tile shared by
+//          8 waves (bf16, D = 64; above that 2 waves/SIMD cannot hold the registers)
+//   kBase: NB 1, NW 4
+// VDIFF_ATTN_CFG=base|nb2|w8 overrides the choice for A/B measurements.
+enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2 };
+
+AttnCfg pick_cfg(int D, bool bf16, int kind) {
   static const int env = [] {
-    const char* e = getenv("VDIFF_ATTN_NB");
-    return e ? atoi(e) : 0;
+    const char* e = getenv("VDIFF_ATTN_CFG");
+    if (!e) return -1;
+    if (!strcmp(e, "nb2")) return (int)kNB2;
+    if (!strcmp(e, "w8")) return (int)kW8;
+    return (int)kBase;
   }();
-  if (env == 1 || env == 2) return (D == 256 || !bf16) ? 1 : env;
-  if (!bf16 || D == 256) return 1;
-  // dK/dV: NB = 2 spills into the unified register file (256 VGPRs) and measured slower
-  // (D = 64: 38.3 ms vs 34.7 ms at N = 262144); fwd / dQ gain 14% / 12%.
-  if (kind == 2) return 1;
-  return 2;
+  if (!bf16) return kBase;
+  AttnCfg c = kBase;
+  if (env >= 0) c = (AttnCfg)env;
+  else if (D == 64) c = kW8;
+  else if (D == 128 && kind == 0) c = kNB2;  // dQ NB 2 spills at D = 128
+  if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
+  if (c == kW8 && D != 64) c = kBase;
+  return c;
 }
 
-template <typename T, int D, int NB>
+template <typename T, int D, int NB, int NW>
 int fwd_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
                float* lse, hipStream_t st) {
   const size_t lds = tile_loop_lds<T, D, false>();
-  auto kern = attn_fwd_kernel<T, D, NB>;
+  auto kern = attn_fwd_kernel<T, D, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows * NB), (unsigned)d->nseq);
-  kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
-                                    d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
-                                    d->token_stride,
-                                    SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
-                                    d->o_token_stride, d->scale);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
+                                   d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
+                                   d->token_stride,
+                                   SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
+                                   d->o_token_stride, d->scale);
   return vd::check_launch("attn_fwd");
 }
 
 template <typename T, int D>
 int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
              float* lse, hipStream_t st) {
-  if (pick_nb(D, kDMA<T>, 0) == 2) return fwd_launch<T, D, (kDMA<T> && D != 256) ? 2 : 1>(d, q, k, v, o, lse, st);
-  return fwd_launch<T, D, 1>(d, q, k, v, o, lse, st);
+  if constexpr (kDMA<T>) {
+    const AttnCfg c = pick_cfg(D, true, 0);
+    if constexpr (D != 256)
+      if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, q, k, v, o, lse, st);
+    if constexpr (D == 64)
+      if (c == kW8) return fwd_launch<T, D, 1, 8>(d, q, k, v, o, lse, st);
+  }
+  return fwd_launch<T, D, 1, 4>(d, q, k, v, o, lse, st);
 }
 
-template <typename T, int D, int NB>
+template <typename T, int D, int NB, int NW>
 int dq_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-              const void* dout, const float* lse, const float* delta, void* dq, hipStream_t st) {
+              const void* dout, const float* nlse2, const float* ndelta, void* dq,
+              hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const size_t lds = tile_loop_lds<T, D, false>();
-  auto kern = attn_bwd_dq_kernel<T, D, NB>;
+  auto kern = attn_bwd_dq_kernel<T, D, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows * NB), (unsigned)d->nseq);
-  kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
-                                    delta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
-                                    d->o_token_stride, d->scale);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
+                                   ndelta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
+                                   d->o_token_stride, d->scale);
   return vd::check_launch("attn_bwd_dq");
 }
 
@@ -782,34 +905,40 @@ template <typename T, int D>
 int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, const void* o,
                 const void* dout, const float* lse, void* dq, void* ws, hipStream_t st) {
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
-  float* delta = reinterpret_cast<float*>(ws);
   const int64_t rows = (int64_t)d->nseq * d->seq_len;
+  float* ndelta = reinterpret_cast<float*>(ws);  // workspace: [ndelta rows][nlse2 rows]
+  float* nlse2 = ndelta + rows;
   int g = (int)vd_cdiv(rows, 256);
   if (g > 4096) g = 4096;
-  attn_delta_kernel<T, D><<<g, 256, 0, st>>>((const T*)o, (const T*)dout, delta, d->nseq,
-                                              d->seq_len, oa, d->o_token_stride);
+  attn_delta_kernel<T, D><<<g, 256, 0, st>>>((const T*)o, (const T*)dout, lse, ndelta, nlse2,
+                                              d->nseq, d->seq_len, oa, d->o_token_stride);
   int rc = vd::check_launch("attn_delta");
   if (rc) return rc;
-  if (pick_nb(D, kDMA<T>, 1) == 2)
-    return dq_launch<T, D, (kDMA<T> && D != 256) ? 2 : 1>(d, q, k, v, dout, lse, delta, dq, st);
-  return dq_launch<T, D, 1>(d, q, k, v, dout, lse, delta, dq, st);
+  if constexpr (kDMA<T>) {
+    const AttnCfg c = pick_cfg(D, true, 1);
+    if constexpr (D != 256)
+      if (c == kNB2) return dq_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D == 64)
+      if (c == kW8) return dq_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+  }
+  return dq_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
 }
 
-template <typename T, int D, int NB>
+template <typename T, int D, int NB, int NW>
 int dkdv_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                const void* dout, const float* lse, const float* delta, void* dk, void* dv,
+                const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
                 hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   constexpr int DO = D > 128 ? 128 : D;
   const size_t lds = tile_loop_lds<T, D, true>();
-  auto kern = attn_bwd_dkdv_kernel<T, D, DO, NB>;
+  auto kern = attn_bwd_dkdv_kernel<T, D, DO, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, kRows * NB), (unsigned)d->nseq, D / DO);
-  kern<<<grid, kThreads, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse,
-                                    delta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
-                                    d->o_token_stride, d->scale);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq, D / DO);
+  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
+                                   ndelta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
+                                   d->o_token_stride, d->scale);
   return vd::check_launch("attn_bwd_dkdv");
 }
 
@@ -817,11 +946,18 @@ template <typename T, int D>
 int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                   const void* dout, const float* lse, void* dk, void* dv, void* ws,
                   hipStream_t st) {
-  const float* delta = reinterpret_cast<const float*>(ws);
-  // (NB = 2 at D = 128 needs > 512 registers; hipcc 7.2 also crashes on it)
-  if (pick_nb(D, kDMA<T>, 2) == 2)
-    return dkdv_launch<T, D, (kDMA<T> && D <= 64) ? 2 : 1>(d, q, k, v, dout, lse, delta, dk, dv, st);
-  return dkdv_launch<T, D, 1>(d, q, k, v, dout, lse, delta, dk, dv, st);
+  (void)lse;  // read through the workspace copy written by the dQ pass
+  const float* ndelta = reinterpret_cast<const float*>(ws);
+  const float* nlse2 = ndelta + (int64_t)d->nseq * d->seq_len;
+  if constexpr (kDMA<T>) {
+    // (NB = 2 above D = 64 needs > 512 registers; hipcc 7.2 also crashes on it)
+    const AttnCfg c = pick_cfg(D, true, 2);
+    if constexpr (D <= 64)
+      if (c == kNB2) return dkdv_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 64)
+      if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+  }
+  return dkdv_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
 }
 
 #define VD_DISPATCH_HEAD(D_, FN, ...)                        \
@@ -855,7 +991,7 @@ int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const 
 
 size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d) {
   if (!d || d->nseq <= 0 || d->seq_len <= 0) return 0;
-  return (size_t)d->nseq * d->seq_len * sizeof(float) + 256;
+  return 2 * (size_t)d->nseq * d->seq_len * sizeof(float) + 256;  // ndelta, nlse2
 }
 
 int vd_attention_bwd_dq(const vd_attn_desc* d, const void* q, const void* k, const void* v,

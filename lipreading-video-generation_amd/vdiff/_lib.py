@@ -10,7 +10,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvdiff.so")
+# VDIFF_LIB: alternative build of the same library (kernel A/B experiments, tools/)
+LIB_PATH = os.environ.get("VDIFF_LIB") or os.path.join(_HERE, "libvdiff.so")
 
 VD_F32 = 0
 VD_BF16 = 1

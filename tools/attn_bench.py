@@ -70,7 +70,13 @@ if __name__ == "__main__":
     if "--calib" in sys.argv:
         calib()
         sys.argv.remove("--calib")
+    only = None
+    if "--only" in sys.argv:  # --only 64: just the head_dim 64 level
+        i = sys.argv.index("--only")
+        only = int(sys.argv[i + 1])
+        del sys.argv[i:i + 2]
     check()
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     for C, N in ((64, 262144), (128, 65536), (256, 16384)):
-        bench(C, N, reps)
+        if only is None or C == only:
+            bench(C, N, reps)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build an A/B variant of libvdiff.so with extra flags for attention.hip only:
+#   tools/build_variant.sh NAME "-mllvm -flag ..."   ->  lipreading-video-generation_amd/vdiff/libvdiff_NAME.so
+# Run it with VDIFF_LIB=<that path> (vdiff/_lib.py).  Experiments only; the product build is make.
+set -e
+cd "$(dirname "$0")/../lipreading-video-generation_amd/csrc"
+make -s -j8 >/dev/null
+NAME=$1; shift
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function \
+  -munsafe-fp-atomics -I../../include -mllvm -amdgpu-mfma-vgpr-form=1 $@ -c attention.hip \
+  -o build/attention_$NAME.o
+OBJS=$(ls build/*.o | grep -v "attention" | tr '\n' ' ')
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../vdiff/libvdiff_$NAME.so $OBJS build/attention_$NAME.o
+echo ../vdiff/libvdiff_$NAME.so
