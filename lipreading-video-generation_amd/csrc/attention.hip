@@ -479,6 +479,78 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
   }
 }
 
+// Software-pipelined ring (bf16, D <= 128).  Work is cut into 32-row blocks (two per
+// 64-row tile); per block a kernel has an MFMA step M (this block's S / dP products plus
+// the gradient / PV products of the PREVIOUS block) and a VALU step V (softmax of this
+// block).  Program order per wave is M(0) V(0) M(1) V(1) ... G(last): M(b+1)'s MFMAs do
+// not depend on V(b), so the MFMA pipe and the VALU stay busy together.  With 8 waves the
+// SIMD partners (waves w and w+4) take the tile barrier at different points of that
+// sequence -- waves 0-3 run [M V M V] between barriers, waves 4-7 [V M V M] -- so one
+// partner's MFMAs run beside the other's softmax instead of in lockstep with it.
+// Four stages, prefetch distance 2: tiles t and t-1 are read while t+1, t+2 land.
+template <typename T> struct BlockRef {
+  const T* a;       // stream a rows of the block's tile (K for fwd / dQ, Q for dK/dV)
+  const T* b;       // stream b rows (V, or dO)
+  const float* rc;  // row constants of the tile (dK/dV)
+  int row0;         // 0 or 32: the block's rows within its tile
+  int idx;          // block index: rows [32 idx, 32 idx + 32) of the sequence
+};
+
+template <typename T, int D, bool RC, int NW, typename MF, typename VF>
+__device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, int64_t ts_a,
+                                          int64_t ts_b, const float* rc0, const float* rc1,
+                                          int n, int tid, bool late, MF&& M, VF&& V) {
+  static_assert(kDMA<T> && D <= 128, "pipelined ring: bf16, D <= 128");
+  constexpr int TE = tile_elems<T, D>();
+  constexpr int NST = 4, PD = 2;
+  constexpr int STAGE_BYTES = 2 * TE * 2 + (RC ? 768 : 0);
+  constexpr int PER_TILE = 2 * dma_ipw<D, NW>() + (RC ? 1 : 0);
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntiles = (n + kTile - 1) / kTile;
+  const auto ra = make_rsrc(a, seq_bytes(n, ts_a, D, 2));
+  const auto rb = make_rsrc(b, seq_bytes(n, ts_b, D, 2));
+  rsrc_t r0, r1;
+  if constexpr (RC) {
+    r0 = make_rsrc(rc0, (uint32_t)n * 4u);
+    r1 = make_rsrc(rc1, (uint32_t)n * 4u);
+  }
+  const uint32_t tsa = (uint32_t)(ts_a * 2), tsb = (uint32_t)(ts_b * 2);
+  auto issue = [&](int t) {
+    char* st = smem + (t % NST) * STAGE_BYTES;
+    const int tok0 = t * kTile;
+    dma_tile<D, NW>(ra, st, tok0, n, tsa, wave, lane);
+    dma_tile<D, NW>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
+    if constexpr (RC) {
+      char* rcs = st + 4 * TE + (wave < 2 ? wave * 256 : 512);
+      dma_rowc(wave == 1 ? r1 : r0, rcs, tok0, lane);
+    }
+  };
+  auto blk = [&](int bi) {
+    const char* st = smem + ((bi >> 1) % NST) * STAGE_BYTES;
+    return BlockRef<T>{reinterpret_cast<const T*>(st), reinterpret_cast<const T*>(st + TE * 2),
+                       reinterpret_cast<const float*>(st + 4 * TE), 32 * (bi & 1), bi};
+  };
+  vm_drain();
+#pragma unroll
+  for (int s = 0; s < PD; ++s) issue(s);
+  for (int t = 0; t < ntiles; ++t) {
+    vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
+    issue(t + PD);
+    if (late && t > 0) V(blk(2 * t - 1));
+    M(blk(2 * t), true, blk(2 * t - 1), t > 0);
+    V(blk(2 * t));
+    M(blk(2 * t + 1), true, blk(2 * t), true);
+    if (!late) V(blk(2 * t + 1));
+  }
+  if (late) V(blk(2 * ntiles - 1));
+  M(blk(2 * ntiles - 1), false, blk(2 * ntiles - 1), true);
+  vm_drain();
+}
+
+template <int D, bool RC>
+constexpr size_t tile_pipe_lds() { return 4 * (size_t)(2 * kTile * D * 2 + (RC ? 768 : 0)); }
+
 template <typename T, int D, bool RC>
 size_t tile_loop_lds() {
   if constexpr (kDMA<T>) return (size_t)nstage<D>() * (2 * tile_elems<T, D>() * 2 + (RC ? 768 : 0));
@@ -504,7 +576,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
@@ -666,7 +738,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_kernel(
     const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
     T* __restrict__ dq, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
@@ -739,7 +811,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
     T* __restrict__ dk, T* __restrict__ dv, int n, SeqAddr qa, int64_t ts, SeqAddr oa,
     int64_t ots, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int seq = blockIdx.y;
   const int d0 = blockIdx.z * DO;
   const int k0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
@@ -815,6 +887,204 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
   }
 }
 
+// ================================================================== pipelined kernels
+// Same math as the kernels above (one 32-row block per wave, NB = 1), on tile_pipe.
+
+template <typename T, int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
+    float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
+  const int seq = blockIdx.y;
+  const int q0 = blockIdx.x * (32 * NW) + wave * 32;
+  const int64_t base = qa(seq);
+  const bool late = NW == 8 && wave >= 4;
+
+  RowFrag<T, D> qf;
+  qf.load(q + base, ts, q0 + (lane & 31), n, lane);
+  qf.scale(scale * kLog2e);
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+  f32x16 negm, s;
+  XOp<T> p;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negm[r] = INFINITY;
+
+  auto mask = [&](int key0) {
+    if (key0 + 32 > n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (key0 + acc_row(r, hh) >= n) s[r] = -INFINITY;
+  };
+  tile_pipe<T, D, false, NW>(
+      smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
+      [&](const BlockRef<T>& bs, bool doS, const BlockRef<T>& bg, bool doG) {
+        if (doS) {
+          s = negm;
+          mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
+        }
+        if (doG)
+#pragma unroll
+          for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], bg.b, bg.row0, 32 * i, p, lane);
+      },
+      [&](const BlockRef<T>& bv) {
+        mask(32 * bv.idx);
+        float psum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s[r] = fast_exp2(s[r]);
+          psum += s[r];
+        }
+        if (!__all(psum < kLagSum)) {  // rare: redo the block against its true max
+          s = f32x16{};
+          mma_rows<T, D>(s, bv.a, bv.row0, qf, lane);
+          mask(32 * bv.idx);
+          float tmax = s[0];
+#pragma unroll
+          for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, s[r]);
+          tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+          const float mnew = fmaxf(m, tmax);
+          const float alpha = fast_exp2(m - mnew);
+          m = mnew;
+          l *= alpha;
+#pragma unroll
+          for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) negm[r] = -mnew;
+          psum = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            s[r] = fast_exp2(s[r] - mnew);
+            psum += s[r];
+          }
+        }
+        l += psum;
+        p = XOp<T>(s);
+      });
+  const int myq = q0 + (lane & 31);
+  const float lt = l + __shfl_xor(l, 32, 64);
+  store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, oacc, 1.f / lt, lane);
+  if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m + log2f(lt)) / kLog2e;
+}
+
+template <typename T, int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
+    const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
+    T* __restrict__ dq, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int seq = blockIdx.y;
+  const int q0 = blockIdx.x * (32 * NW) + wave * 32;
+  const int64_t base = qa(seq);
+  const bool late = NW == 8 && wave >= 4;
+
+  RowFrag<T, D> qf, of;
+  f32x16 il, id;
+  {
+    const int myq = q0 + (lane & 31);
+    qf.load(q + base, ts, myq, n, lane);
+    qf.scale(scale * kLog2e);
+    of.load(dout + oa(seq), ots, myq, n, lane);
+    const float a = myq < n ? nlse2[(int64_t)seq * n + myq] : 0.f;
+    const float b = myq < n ? ndelta[(int64_t)seq * n + myq] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      il[r] = a;
+      id[r] = b;
+    }
+  }
+  f32x16 acc[D / 32], s, dp;
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) acc[i] = f32x16{};
+  XOp<T> ds;
+
+  tile_pipe<T, D, false, NW>(
+      smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
+      [&](const BlockRef<T>& bs, bool doS, const BlockRef<T>& bg, bool doG) {
+        if (doS) {
+          s = il;
+          dp = id;
+          mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
+          mma_rows<T, D>(dp, bs.b, bs.row0, of, lane);
+        }
+        if (doG)  // dQ^T += K^T dS^T (keys past n: zero K rows)
+#pragma unroll
+          for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(acc[i], bg.a, bg.row0, 32 * i, ds, lane);
+      },
+      [&](const BlockRef<T>&) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = fast_exp2(s[r]) * dp[r];
+        ds = XOp<T>(s);
+      });
+  store_transposed<T, D / 32>(dq + base, ts, q0 + (lane & 31), n, 0, acc, scale, lane);
+}
+
+template <typename T, int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
+    const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
+    T* __restrict__ dk, T* __restrict__ dv, int n, SeqAddr qa, int64_t ts, SeqAddr oa,
+    int64_t ots, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
+  const int seq = blockIdx.y;
+  const int k0 = blockIdx.x * (32 * NW) + wave * 32;
+  const int64_t base = qa(seq), obase = oa(seq);
+  const bool late = NW == 8 && wave >= 4;
+
+  RowFrag<T, D> kf, vf;
+  kf.load(k + base, ts, k0 + (lane & 31), n, lane);
+  kf.scale(scale * kLog2e);
+  vf.load(v + base, ts, k0 + (lane & 31), n, lane);
+  f32x16 adv[D / 32], adk[D / 32], s, dp;
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) adv[i] = adk[i] = f32x16{};
+  XOp<T> pp, ds;
+
+  tile_pipe<T, D, true, NW>(
+      smem, q + base, dout + obase, ts, ots, nlse2 + (int64_t)seq * n, ndelta + (int64_t)seq * n,
+      n, tid, late,
+      [&](const BlockRef<T>& bs, bool doS, const BlockRef<T>& bg, bool doG) {
+        if (doS) {
+          // registers 4g..4g+3 are query rows 8g + 4hh + 0..3 of the block
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 ls = *reinterpret_cast<const float4*>(bs.rc + bs.row0 + 8 * g + 4 * hh);
+            const float4 dl =
+                *reinterpret_cast<const float4*>(bs.rc + 64 + bs.row0 + 8 * g + 4 * hh);
+            s[4 * g + 0] = ls.x; s[4 * g + 1] = ls.y; s[4 * g + 2] = ls.z; s[4 * g + 3] = ls.w;
+            dp[4 * g + 0] = dl.x; dp[4 * g + 1] = dl.y; dp[4 * g + 2] = dl.z; dp[4 * g + 3] = dl.w;
+          }
+          mma_rows<T, D>(s, bs.a, bs.row0, kf, lane);   // S'[q][key] - lse'
+          mma_rows<T, D>(dp, bs.b, bs.row0, vf, lane);  // dP[q][key] - delta
+        }
+        if (doG)
+#pragma unroll
+          for (int i = 0; i < D / 32; ++i) {
+            mma_tr<T, D>(adv[i], bg.b, bg.row0, 32 * i, pp, lane);  // dV^T += dO^T P
+            mma_tr<T, D>(adk[i], bg.a, bg.row0, 32 * i, ds, lane);  // dK^T += Q^T dS
+          }
+      },
+      [&](const BlockRef<T>&) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s[r] = fast_exp2(s[r]);
+          dp[r] *= s[r];
+        }
+        pp = XOp<T>(s);
+        ds = XOp<T>(dp);
+      });
+  const int mykey = k0 + (lane & 31);
+  store_transposed<T, D / 32>(dk + base, ts, mykey, n, 0, adk, scale, lane);
+  store_transposed<T, D / 32>(dv + base, ts, mykey, n, 0, adv, 1.f, lane);
+}
+
 // ------------------------------------------------------------------ launchers
 int check_attn(const vd_attn_desc* d) {
   VD_REQUIRE(d, "null descriptor");
@@ -834,8 +1104,10 @@ int check_attn(const vd_attn_desc* d) {
 //   kW8  : NB 1, NW 8 -- two waves per SIMD from one workgroup, each LDS tile shared by
 //          8 waves (bf16, D = 64; above that 2 waves/SIMD cannot hold the registers)
 //   kBase: NB 1, NW 4
-// VDIFF_ATTN_CFG=base|nb2|w8 overrides the choice for A/B measurements.
-enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2 };
+// VDIFF_ATTN_CFG=base|nb2|w8|p8|p4 overrides the choice for A/B measurements.
+//   kP8 / kP4: the software-pipelined kernels (tile_pipe) with 8 / 4 waves (bf16, D <= 128;
+//          8 waves only at D = 64)
+enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4 };
 
 AttnCfg pick_cfg(int D, bool bf16, int kind) {
   static const int env = [] {
@@ -843,15 +1115,22 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
     if (!e) return -1;
     if (!strcmp(e, "nb2")) return (int)kNB2;
     if (!strcmp(e, "w8")) return (int)kW8;
+    if (!strcmp(e, "p8")) return (int)kP8;
+    if (!strcmp(e, "p4")) return (int)kP4;
     return (int)kBase;
   }();
   if (!bf16) return kBase;
   AttnCfg c = kBase;
+  // defaults = the fastest measured (tools/attn_bench.py, MI355X):
+  //   D = 64 : fwd W8 17.5 ms, dQ P8 22.3 ms, dK/dV W8 29.3 ms (N = 262144)
+  //   D = 128: fwd NB2 2.0 ms, dQ P4 3.5 ms, dK/dV base 4.6 ms (N = 65536)
   if (env >= 0) c = (AttnCfg)env;
-  else if (D == 64) c = kW8;
-  else if (D == 128 && kind == 0) c = kNB2;  // dQ NB 2 spills at D = 128
+  else if (D == 64) c = kind == 1 ? kP8 : kW8;
+  else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kP4 : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64) c = kBase;
+  if (c == kP8 && D != 64) c = kP4;
+  if (c == kP4 && D > 128) c = kBase;
   return c;
 }
 
@@ -871,6 +1150,22 @@ int fwd_launch(const vd_attn_desc* d, const void* q, const void* k, const void* 
   return vd::check_launch("attn_fwd");
 }
 
+template <typename T, int D, int NW>
+int fwd_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
+                    float* lse, hipStream_t st) {
+  const size_t lds = tile_pipe_lds<D, false>();
+  auto kern = attn_fwd_pipe_kernel<T, D, NW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
+                                   d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
+                                   d->token_stride,
+                                   SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
+                                   d->o_token_stride, d->scale);
+  return vd::check_launch("attn_fwd");
+}
+
 template <typename T, int D>
 int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
              float* lse, hipStream_t st) {
@@ -880,6 +1175,10 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
       if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, q, k, v, o, lse, st);
     if constexpr (D == 64)
       if (c == kW8) return fwd_launch<T, D, 1, 8>(d, q, k, v, o, lse, st);
+    if constexpr (D == 64)
+      if (c == kP8) return fwd_pipe_launch<T, D, 8>(d, q, k, v, o, lse, st);
+    if constexpr (D <= 128)
+      if (c == kP4) return fwd_pipe_launch<T, D, 4>(d, q, k, v, o, lse, st);
   }
   return fwd_launch<T, D, 1, 4>(d, q, k, v, o, lse, st);
 }
@@ -895,6 +1194,23 @@ int dq_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
+                                   ndelta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
+                                   d->o_token_stride, d->scale);
+  return vd::check_launch("attn_bwd_dq");
+}
+
+template <typename T, int D, int NW>
+int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                   const void* dout, const float* nlse2, const float* ndelta, void* dq,
+                   hipStream_t st) {
+  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+  const size_t lds = tile_pipe_lds<D, false>();
+  auto kern = attn_bwd_dq_pipe_kernel<T, D, NW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW), (unsigned)d->nseq);
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
                                    ndelta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
                                    d->o_token_stride, d->scale);
@@ -920,6 +1236,10 @@ int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void*
       if (c == kNB2) return dq_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kW8) return dq_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D == 64)
+      if (c == kP8) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D <= 128)
+      if (c == kP4) return dq_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
   }
   return dq_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
 }
@@ -942,6 +1262,23 @@ int dkdv_launch(const vd_attn_desc* d, const void* q, const void* k, const void*
   return vd::check_launch("attn_bwd_dkdv");
 }
 
+template <typename T, int D, int NW>
+int dkdv_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                     const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
+                     hipStream_t st) {
+  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+  const size_t lds = tile_pipe_lds<D, true>();
+  auto kern = attn_bwd_dkdv_pipe_kernel<T, D, NW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
+                                   ndelta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
+                                   d->o_token_stride, d->scale);
+  return vd::check_launch("attn_bwd_dkdv");
+}
+
 template <typename T, int D>
 int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                   const void* dout, const float* lse, void* dk, void* dv, void* ws,
@@ -956,6 +1293,10 @@ int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const voi
       if (c == kNB2) return dkdv_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 64)
+      if (c == kP8) return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D <= 128)
+      if (c == kP4) return dkdv_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
   }
   return dkdv_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
 }
