@@ -32,6 +32,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 namespace {
 
 // A workgroup is NW waves (4 or 8); each wave owns NB x 32 rows (queries for fwd / dQ,
@@ -39,6 +41,21 @@ namespace {
 // among its NW waves.
 constexpr int kTile = 64;      // keys (fwd, dQ) or queries (dKdV) per LDS tile
 constexpr float kLog2e = 1.4426950408889634f;
+
+// Diagnostic build only (-DVD_ATTN_STAMPS, tools/attn_stamps.py): s_memtime stamps of
+// lane 0 of every wave of workgroups 0..63 (grid row 0) for the first 64 tiles.
+#ifdef VD_ATTN_STAMPS
+__device__ unsigned long long g_stamps[64][8][4][64];
+#define VD_STAMP(kind, t)                                                                   \
+  do {                                                                                      \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 64 && blockIdx.y == 0 && (t) < 64)         \
+      g_stamps[blockIdx.x][threadIdx.x >> 6][kind][t] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+#else
+#define VD_STAMP(kind, t) \
+  do {                    \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------ LDS tiles
 // bf16 tile [64][D]: 16-B chunks XOR-swizzled per row.  Two read shapes must both be
@@ -275,6 +292,33 @@ __device__ __forceinline__ void mma_tr_nb(f32x16 (&acc)[NB], const T* tile, int 
   }
 }
 
+// The two k16 A-operand steps of tile[sum0 .. sum0+32][col0 .. col0+32]^T (as mma_tr reads
+// them), into registers.
+template <int D>
+__device__ __forceinline__ void load_tr(bf16x8 (&f)[2], const bf16_t* tile, int sum0, int col0,
+                                        int lane) {
+  const int g = lane >> 4, fr = lane & 15;
+  const int q4 = fr >> 2, p4 = fr & 3;
+  const int col = col0 + 16 * (g & 1) + 4 * p4;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int kr = sum0 + 16 * s2 + 4 * (g >> 1) + q4;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4*)(tile + toff<bf16_t, D>(kr, col)));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4*)(tile + toff<bf16_t, D>(kr + 8, col)));
+    f[s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+template <int D>
+__device__ __forceinline__ void load_tr(bf16x8 (&f)[2], const float*, int, int, int) {}
+
+#ifdef VD_ATTN_NOPRELOAD
+constexpr bool kPreload = false;
+#else
+constexpr bool kPreload = true;
+#endif
+
 // v_exp_f32 directly (inputs here are <= 0 or -inf; no range reduction needed)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -425,11 +469,14 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
 #pragma unroll
     for (int s = 0; s < NST - 1; ++s) issue(s);
     for (int t = 0; t < ntiles; ++t) {
+      VD_STAMP(0, t);
       vm_wait_barrier<(NST - 2) * PER_TILE>();
+      VD_STAMP(1, t);
       issue(t + NST - 1);  // beyond the end: fully out-of-range rows (zero fill, no traffic)
       const char* st = smem + (t % NST) * STAGE_BYTES;
       body(t, reinterpret_cast<const T*>(st), reinterpret_cast<const T*>(st + TE * 2),
            reinterpret_cast<const float*>(st + 4 * TE));
+      VD_STAMP(3, t);
     }
     vm_drain();
   } else {
@@ -488,6 +535,8 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
 // sequence -- waves 0-3 run [M V M V] between barriers, waves 4-7 [V M V M] -- so one
 // partner's MFMAs run beside the other's softmax instead of in lockstep with it.
 // Four stages, prefetch distance 2: tiles t and t-1 are read while t+1, t+2 land.
+// S(b): the block's S / dP products; G(b): its gradient / PV products (needs V(b));
+// V(b): its softmax.  Order: S(2t) G(2t-1) V(2t) S(2t+1) G(2t) V(2t+1).
 template <typename T> struct BlockRef {
   const T* a;       // stream a rows of the block's tile (K for fwd / dQ, Q for dK/dV)
   const T* b;       // stream b rows (V, or dO)
@@ -496,10 +545,31 @@ template <typename T> struct BlockRef {
   int idx;          // block index: rows [32 idx, 32 idx + 32) of the sequence
 };
 
-template <typename T, int D, bool RC, int NW, typename MF, typename VF>
+// Optional instruction-group schedule for one block (IGroupLP sched_group_barrier):
+// SR LDS reads, SM MFMAs (S), GR LDS reads, then GM x {1 MFMA (G), VP VALU (softmax)}.
+// All zero: leave the order to the compiler.
+template <int SR, int SM, int GR, int GM, int VP> struct BlockSched {
+  static constexpr bool on = SM > 0;
+  __device__ __forceinline__ static void emit() {
+    if constexpr (SM > 0) {
+      __builtin_amdgcn_sched_group_barrier(0x100, SR, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, SM, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);
+#pragma unroll
+      for (int i = 0; i < GM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, VP, 0);
+      }
+    }
+  }
+};
+using NoSched = BlockSched<0, 0, 0, 0, 0>;
+
+template <typename T, int D, bool RC, int NW, typename SCH = NoSched, typename SF, typename GF,
+          typename VF>
 __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, int64_t ts_a,
                                           int64_t ts_b, const float* rc0, const float* rc1,
-                                          int n, int tid, bool late, MF&& M, VF&& V) {
+                                          int n, int tid, bool late, SF&& S, GF&& G, VF&& V) {
   static_assert(kDMA<T> && D <= 128, "pipelined ring: bf16, D <= 128");
   constexpr int TE = tile_elems<T, D>();
   constexpr int NST = 4, PD = 2;
@@ -527,29 +597,50 @@ __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, in
     }
   };
   auto blk = [&](int bi) {
-    const char* st = smem + ((bi >> 1) % NST) * STAGE_BYTES;
+    const char* st = smem + ((bi >> 1) & (NST - 1)) * STAGE_BYTES;
     return BlockRef<T>{reinterpret_cast<const T*>(st), reinterpret_cast<const T*>(st + TE * 2),
                        reinterpret_cast<const float*>(st + 4 * TE), 32 * (bi & 1), bi};
   };
+  // Stage NST-1 stands in for tile -1: zeroed, so G(-1) (the previous block's products at
+  // t = 0) reads zero rows and adds nothing -- the loop body needs no t > 0 branch.
+  {
+    uint4* z = reinterpret_cast<uint4*>(smem + (NST - 1) * STAGE_BYTES);
+    for (int i = tid; i < STAGE_BYTES / 16; i += 64 * NW) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
   vm_drain();
 #pragma unroll
   for (int s = 0; s < PD; ++s) issue(s);
-  for (int t = 0; t < ntiles; ++t) {
-    vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
-    issue(t + PD);
-    if (late && t > 0) V(blk(2 * t - 1));
-    M(blk(2 * t), true, blk(2 * t - 1), t > 0);
-    V(blk(2 * t));
-    M(blk(2 * t + 1), true, blk(2 * t), true);
-    if (!late) V(blk(2 * t + 1));
-  }
-  if (late) V(blk(2 * ntiles - 1));
-  M(blk(2 * ntiles - 1), false, blk(2 * ntiles - 1), true);
+  // One loop copy per wave role, so each tile's body is one basic block (MFMA and VALU
+  // of neighbouring steps can interleave in the schedule).
+  auto run = [&](auto late_c) {
+    constexpr bool LATE = decltype(late_c)::value;
+    for (int t = 0; t < ntiles; ++t) {
+      vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
+      issue(t + PD);
+      if constexpr (LATE) V(blk(2 * t - 1));
+      S(blk(2 * t));
+      G(blk(2 * t - 1));
+      V(blk(2 * t));
+      S(blk(2 * t + 1));
+      G(blk(2 * t));
+      if constexpr (!LATE) V(blk(2 * t + 1));
+      if constexpr (SCH::on && !LATE) {
+        SCH::emit();
+        SCH::emit();
+      }
+    }
+    if constexpr (LATE) V(blk(2 * ntiles - 1));
+    G(blk(2 * ntiles - 1));
+  };
+  if (late) run(std::true_type{});
+  else run(std::false_type{});
   vm_drain();
 }
 
 template <int D, bool RC>
 constexpr size_t tile_pipe_lds() { return 4 * (size_t)(2 * kTile * D * 2 + (RC ? 768 : 0)); }
+
 
 template <typename T, int D, bool RC>
 size_t tile_loop_lds() {
@@ -616,11 +707,38 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
             for (int j = 0; j < NB; ++j) s[h][j][r] = -INFINITY;
     };
     f32x16 s[2][NB];
+    // NB = 1, bf16: every LDS fragment of the tile is read up front (K rows for S', V^T for
+    // PV; 64 VGPRs), so no MFMA waits on a just-issued read
+    constexpr bool kPre = kDMA<T> && NB == 1 && D <= 64 && kPreload;
+    bf16x8 kfr[2][D / 16];
+    bf16x8 vfr[D / 32][2][2];
+    if constexpr (kPre) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int j = 0; j < NB; ++j) s[h][j] = negm[j];
-      mma_rows_nb<T, D, NB>(s[h], Kt, 32 * h, qf, lane);
+        for (int ss = 0; ss < D / 16; ++ss)
+          kfr[h][ss] = *reinterpret_cast<const bf16x8*>(
+              Kt + toff<T, D>(32 * h + (lane & 31), 16 * ss + 8 * hh));
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) load_tr<D>(vfr[i][h], Vt, 32 * h, 32 * i, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        s[h][0] = negm[0];
+#pragma unroll
+        for (int ss = 0; ss < D / 16; ++ss)
+          s[h][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[h][ss], qf[0].f[ss], s[h][0],
+                                                            0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) s[h][j] = negm[j];
+        mma_rows_nb<T, D, NB>(s[h], Kt, 32 * h, qf, lane);
+      }
     }
     if (tail) mask(s);
     float psum[NB];
@@ -638,6 +756,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
         }
       ok = ok && psum[j] < kLagSum;  // false for inf / NaN too
     }
+    VD_STAMP(2, t);
     if (!__all(ok)) {  // rare: recompute S' with the true max of this tile
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -682,10 +801,21 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
 #pragma unroll
       for (int h = 0; h < 2; ++h) p[h][j] = XOp<T>(s[h][j]);
     }
+    if constexpr (kPre) {
 #pragma unroll
-    for (int i = 0; i < D / 32; ++i) {
-      mma_tr_nb<T, D, NB>(oacc[i], Vt, 0, 32 * i, p[0], lane);
-      mma_tr_nb<T, D, NB>(oacc[i], Vt, 32, 32 * i, p[1], lane);
+      for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            oacc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[i][h][s2], p[h][0].b[s2],
+                                                                 oacc[i][0], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i) {
+        mma_tr_nb<T, D, NB>(oacc[i], Vt, 0, 32 * i, p[0], lane);
+        mma_tr_nb<T, D, NB>(oacc[i], Vt, 32, 32 * i, p[1], lane);
+      }
     }
   });
 #pragma unroll
@@ -888,6 +1018,16 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
 }
 
 // ================================================================== pipelined kernels
+#ifdef VD_ATTN_SCHED
+constexpr bool kSchedOn = true;
+#else
+constexpr bool kSchedOn = false;
+#endif
+// per block: LDS reads / MFMAs of S, LDS reads of G, G MFMAs with the softmax VALU spread
+template <int D> using DkdvSched = BlockSched<16, 8, 4 * D / 16, D / 8, 48 / (D / 8)>;
+template <int D> using DqSched = BlockSched<8, 8, D / 8, D / 16, 40 / (D / 16)>;
+
+
 // Same math as the kernels above (one 32-row block per wave, NB = 1), on tile_pipe.
 
 template <typename T, int D, int NW>
@@ -909,9 +1049,12 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
   for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
   float m = -INFINITY, l = 0.f;
   f32x16 negm, s;
-  XOp<T> p;
+  XOp<T> p{};  // zero: the G step before the first softmax adds nothing
 #pragma unroll
-  for (int r = 0; r < 16; ++r) negm[r] = INFINITY;
+  for (int r = 0; r < 16; ++r) {
+    negm[r] = INFINITY;
+    s[r] = -INFINITY;  // a late wave's V(-1) then yields p = 0, psum = 0
+  }
 
   auto mask = [&](int key0) {
     if (key0 + 32 > n)
@@ -921,14 +1064,13 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
   };
   tile_pipe<T, D, false, NW>(
       smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
-      [&](const BlockRef<T>& bs, bool doS, const BlockRef<T>& bg, bool doG) {
-        if (doS) {
-          s = negm;
-          mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
-        }
-        if (doG)
+      [&](const BlockRef<T>& bs) {
+        s = negm;
+        mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
+      },
+      [&](const BlockRef<T>& bg) {
 #pragma unroll
-          for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], bg.b, bg.row0, 32 * i, p, lane);
+        for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], bg.b, bg.row0, 32 * i, p, lane);
       },
       [&](const BlockRef<T>& bv) {
         mask(32 * bv.idx);
@@ -999,23 +1141,22 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
       id[r] = b;
     }
   }
-  f32x16 acc[D / 32], s, dp;
+  f32x16 acc[D / 32], s{}, dp{};
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) acc[i] = f32x16{};
-  XOp<T> ds;
+  XOp<T> ds{};
 
-  tile_pipe<T, D, false, NW>(
+  tile_pipe<T, D, false, NW, typename std::conditional<kSchedOn, DqSched<D>, NoSched>::type>(
       smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
-      [&](const BlockRef<T>& bs, bool doS, const BlockRef<T>& bg, bool doG) {
-        if (doS) {
-          s = il;
-          dp = id;
-          mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
-          mma_rows<T, D>(dp, bs.b, bs.row0, of, lane);
-        }
-        if (doG)  // dQ^T += K^T dS^T (keys past n: zero K rows)
+      [&](const BlockRef<T>& bs) {
+        s = il;
+        dp = id;
+        mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
+        mma_rows<T, D>(dp, bs.b, bs.row0, of, lane);
+      },
+      [&](const BlockRef<T>& bg) {  // dQ^T += K^T dS^T (keys past n: zero K rows)
 #pragma unroll
-          for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(acc[i], bg.a, bg.row0, 32 * i, ds, lane);
+        for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(acc[i], bg.a, bg.row0, 32 * i, ds, lane);
       },
       [&](const BlockRef<T>&) {
 #pragma unroll
@@ -1042,34 +1183,32 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   kf.load(k + base, ts, k0 + (lane & 31), n, lane);
   kf.scale(scale * kLog2e);
   vf.load(v + base, ts, k0 + (lane & 31), n, lane);
-  f32x16 adv[D / 32], adk[D / 32], s, dp;
+  f32x16 adv[D / 32], adk[D / 32], s{}, dp{};
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) adv[i] = adk[i] = f32x16{};
-  XOp<T> pp, ds;
+  XOp<T> pp{}, ds{};
 
-  tile_pipe<T, D, true, NW>(
+  tile_pipe<T, D, true, NW, typename std::conditional<kSchedOn, DkdvSched<D>, NoSched>::type>(
       smem, q + base, dout + obase, ts, ots, nlse2 + (int64_t)seq * n, ndelta + (int64_t)seq * n,
       n, tid, late,
-      [&](const BlockRef<T>& bs, bool doS, const BlockRef<T>& bg, bool doG) {
-        if (doS) {
-          // registers 4g..4g+3 are query rows 8g + 4hh + 0..3 of the block
+      [&](const BlockRef<T>& bs) {
+        // registers 4g..4g+3 are query rows 8g + 4hh + 0..3 of the block
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const float4 ls = *reinterpret_cast<const float4*>(bs.rc + bs.row0 + 8 * g + 4 * hh);
-            const float4 dl =
-                *reinterpret_cast<const float4*>(bs.rc + 64 + bs.row0 + 8 * g + 4 * hh);
-            s[4 * g + 0] = ls.x; s[4 * g + 1] = ls.y; s[4 * g + 2] = ls.z; s[4 * g + 3] = ls.w;
-            dp[4 * g + 0] = dl.x; dp[4 * g + 1] = dl.y; dp[4 * g + 2] = dl.z; dp[4 * g + 3] = dl.w;
-          }
-          mma_rows<T, D>(s, bs.a, bs.row0, kf, lane);   // S'[q][key] - lse'
-          mma_rows<T, D>(dp, bs.b, bs.row0, vf, lane);  // dP[q][key] - delta
+        for (int g = 0; g < 4; ++g) {
+          const float4 ls = *reinterpret_cast<const float4*>(bs.rc + bs.row0 + 8 * g + 4 * hh);
+          const float4 dl = *reinterpret_cast<const float4*>(bs.rc + 64 + bs.row0 + 8 * g + 4 * hh);
+          s[4 * g + 0] = ls.x; s[4 * g + 1] = ls.y; s[4 * g + 2] = ls.z; s[4 * g + 3] = ls.w;
+          dp[4 * g + 0] = dl.x; dp[4 * g + 1] = dl.y; dp[4 * g + 2] = dl.z; dp[4 * g + 3] = dl.w;
         }
-        if (doG)
+        mma_rows<T, D>(s, bs.a, bs.row0, kf, lane);   // S'[q][key] - lse'
+        mma_rows<T, D>(dp, bs.b, bs.row0, vf, lane);  // dP[q][key] - delta
+      },
+      [&](const BlockRef<T>& bg) {
 #pragma unroll
-          for (int i = 0; i < D / 32; ++i) {
-            mma_tr<T, D>(adv[i], bg.b, bg.row0, 32 * i, pp, lane);  // dV^T += dO^T P
-            mma_tr<T, D>(adk[i], bg.a, bg.row0, 32 * i, ds, lane);  // dK^T += Q^T dS
-          }
+        for (int i = 0; i < D / 32; ++i) {
+          mma_tr<T, D>(adv[i], bg.b, bg.row0, 32 * i, pp, lane);  // dV^T += dO^T P
+          mma_tr<T, D>(adk[i], bg.a, bg.row0, 32 * i, ds, lane);  // dK^T += Q^T dS
+        }
       },
       [&](const BlockRef<T>&) {
 #pragma unroll
@@ -1122,10 +1261,10 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   if (!bf16) return kBase;
   AttnCfg c = kBase;
   // defaults = the fastest measured (tools/attn_bench.py, MI355X):
-  //   D = 64 : fwd W8 17.5 ms, dQ P8 22.3 ms, dK/dV W8 29.3 ms (N = 262144)
+  //   D = 64 : fwd W8 17.2 ms, dQ P8 21.6 ms, dK/dV P8 29.1 ms (N = 262144)
   //   D = 128: fwd NB2 2.0 ms, dQ P4 3.5 ms, dK/dV base 4.6 ms (N = 65536)
   if (env >= 0) c = (AttnCfg)env;
-  else if (D == 64) c = kind == 1 ? kP8 : kW8;
+  else if (D == 64) c = kind == 0 ? kW8 : kP8;
   else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kP4 : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64) c = kBase;
@@ -1313,6 +1452,16 @@ int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const voi
 }  // namespace
 
 extern "C" {
+
+#ifdef VD_ATTN_STAMPS
+int vd_debug_attn_stamps(void* dst, size_t bytes) {
+  if (bytes > sizeof(g_stamps)) bytes = sizeof(g_stamps);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : 1;
+}
+#endif
 
 int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
                      float* lse, void* stream) {
