@@ -208,6 +208,12 @@ typedef struct vd_attn_desc {
 int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k,
                      const void* v, void* o, float* lse, void* stream);
 size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d);
+/* Kernel shape used for bf16 (no effect on results beyond fp32 summation order):
+ * -1 per-kernel default, 0 base (4 waves x 32 rows), 1 two 32-row blocks per wave,
+ * 2 eight waves, 3 / 4 software-pipelined with 8 / 4 waves.  Process-wide; returns the
+ * previous setting, or -2 for an invalid cfg (vd_last_error says why).  Initial value from env VDIFF_ATTN_CFG
+ * (base|nb2|w8|p8|p4).  No reference counterpart: an A/B and test hook. */
+int vd_attention_set_config(int cfg);
 /* dout uses the o_* strides; dq/dk/dv use the q/k/v strides (so they can be
  * written straight into a d(qkv) buffer) and are OVERWRITTEN. */
 int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k,
@@ -215,8 +221,8 @@ int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k,
                      const float* lse, void* dq, void* dk, void* dv,
                      void* workspace, void* stream);
 /* The two halves of vd_attention_bwd (same arguments), for per-kernel timing:
- * _dq writes delta = rowsum(dO * O) into the workspace and computes dq;
- * _dkdv reads that delta and computes dk, dv.  Call _dq first. */
+ * _dq writes the per-row constants -rowsum(dO * O) and -lse*log2(e) into the
+ * workspace and computes dq; _dkdv reads them and computes dk, dv.  Call _dq first. */
 int vd_attention_bwd_dq(const vd_attn_desc* d, const void* q, const void* k,
                         const void* v, const void* o, const void* dout,
                         const float* lse, void* dq, void* workspace,

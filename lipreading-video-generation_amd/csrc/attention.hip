@@ -32,6 +32,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <type_traits>
 
 namespace {
@@ -1248,16 +1249,20 @@ int check_attn(const vd_attn_desc* d) {
 //          8 waves only at D = 64)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4 };
 
+int cfg_from_env() {
+  const char* e = getenv("VDIFF_ATTN_CFG");
+  if (!e) return -1;
+  if (!strcmp(e, "nb2")) return (int)kNB2;
+  if (!strcmp(e, "w8")) return (int)kW8;
+  if (!strcmp(e, "p8")) return (int)kP8;
+  if (!strcmp(e, "p4")) return (int)kP4;
+  if (!strcmp(e, "base")) return (int)kBase;
+  return -1;
+}
+std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
+
 AttnCfg pick_cfg(int D, bool bf16, int kind) {
-  static const int env = [] {
-    const char* e = getenv("VDIFF_ATTN_CFG");
-    if (!e) return -1;
-    if (!strcmp(e, "nb2")) return (int)kNB2;
-    if (!strcmp(e, "w8")) return (int)kW8;
-    if (!strcmp(e, "p8")) return (int)kP8;
-    if (!strcmp(e, "p4")) return (int)kP4;
-    return (int)kBase;
-  }();
+  const int env = g_cfg.load(std::memory_order_relaxed);
   if (!bf16) return kBase;
   AttnCfg c = kBase;
   // defaults = the fastest measured (tools/attn_bench.py, MI355X):
@@ -1477,6 +1482,14 @@ int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const 
     VD_DISPATCH_HEAD(d->head_dim, fwd_impl, d, q, k, v, o, lse, st);
   }
   return vd::fail(VD_EUNSUPPORTED, "dtype %d", d->dtype);
+}
+
+int vd_attention_set_config(int cfg) {
+  if (cfg < -1 || cfg > (int)kP4) {
+    (void)vd::fail(VD_EINVAL, "attention config %d", cfg);
+    return -2;
+  }
+  return g_cfg.exchange(cfg);
 }
 
 size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d) {

@@ -66,6 +66,7 @@ _SIGS = {
     "vd_conv3d_bwd_weight": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp]),
     "vd_attention_fwd": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp]),
     "vd_attention_bwd_workspace_size": (_sz, [C.POINTER(AttnDesc)]),
+    "vd_attention_set_config": (C.c_int, [C.c_int]),
     "vd_attention_bwd": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                               _vp, _vp]),
     "vd_attention_bwd_dq": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

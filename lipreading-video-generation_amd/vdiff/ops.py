@@ -571,6 +571,31 @@ class AttentionFn(torch.autograd.Function):
         return dqkv, None, None, None, None
 
 
+ATTN_CONFIGS = {"auto": -1, "base": 0, "nb2": 1, "w8": 2, "p8": 3, "p4": 4}
+
+
+class attention_config:
+    """Context manager selecting the bf16 attention kernel shape (vd_attention_set_config):
+    "auto" (per-kernel default), "base", "nb2", "w8", "p8", "p4".  Results agree across
+    shapes up to fp32 summation order; used by tests and A/B benchmarks."""
+
+    def __init__(self, name: str):
+        if name not in ATTN_CONFIGS:
+            raise ValueError(f"attention config {name!r}: one of {sorted(ATTN_CONFIGS)}")
+        self.cfg = ATTN_CONFIGS[name]
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = _lib.lib().vd_attention_set_config(self.cfg)
+        if self.prev < -1:
+            raise RuntimeError(_lib.lib().vd_last_error().decode())
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().vd_attention_set_config(self.prev)
+        return False
+
+
 def attention(qkv, heads=1, mode="joint", spatial=None, legacy=True):
     if mode != "joint" and spatial is None:
         raise ValueError("spatial/temporal attention needs the (T, H, W) shape")

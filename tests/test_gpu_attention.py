@@ -65,6 +65,45 @@ def test_scores_with_large_logits():
     assert rel_l2(out, ref) < 2e-5
 
 
+CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4"]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+@pytest.mark.parametrize("C", [32, 64, 128, 256])
+def test_bf16_kernel_shapes(cfg, C):
+    """Every bf16 kernel shape (4/8 waves, 1/2 row blocks, software-pipelined ring) on a
+    ragged sequence (N = 201: partial last tile and block) and a sequence shorter than
+    one tile; shapes a head_dim does not support fall back inside the library."""
+    from vdiff import ops
+    with ops.attention_config(cfg):
+        _check(2, C, 1, 3, 67, "joint", True, torch.bfloat16, 60 + C)
+        _check(1, C, 1, 1, 21, "joint", True, torch.bfloat16, 61 + C)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_bf16_lagged_max_rescale(cfg):
+    """bf16 forward with logits that jump late in the sequence: exercises the lagged-max
+    rare path (p reaching 2^16 forces a recompute against the true max)."""
+    from vdiff import ops
+    B, C, N = 1, 64, 1500
+    qkv = seeded((B, 3 * C, N), 52) * 3.0
+    qkv[:, C:2 * C, 1100] *= 12  # one key far above every earlier score, seen late
+    qkv[:, :C, 700] *= 10        # and one query row with a large max of its own
+    qkv = qkv.bfloat16().float()
+    ref = onn.qkv_attention(qkv, 1)
+    with ops.attention_config(cfg):
+        out = ops.attention(ops.to_cl(qkv.to(dev, torch.bfloat16)), heads=1)
+    assert torch.isfinite(out.float()).all()
+    assert rel_l2(out, ref) < 2e-2
+
+
+def test_config_hook_rejects_unknown():
+    from vdiff import _lib, ops
+    assert _lib.lib().vd_attention_set_config(7) == -2
+    with pytest.raises(ValueError):
+        ops.attention_config("fast")
+
+
 def test_golden_regroupings():
     from vdiff import ops
     g = golden("blocks.npz")
