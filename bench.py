@@ -252,6 +252,20 @@ def main():
             f"model {result['model_tflops_per_gpu']} TFLOP/s/GPU (3x fwd)")
         for r in rows:
             log("  kernel", r)
+        conv = timer.conv_summary()
+        by_kind = {}
+        for (kind, key), (cnt, tot, flop) in conv.items():
+            a = by_kind.setdefault(kind, [0, 0.0, 0.0])
+            a[0] += cnt
+            a[1] += tot
+            a[2] += flop * cnt
+        result["conv_kernels"] = {
+            k: {"launches": c, "ms_per_step": round(t / args.steps, 2),
+                "tflops": round(f / (t / 1e3) / 1e12, 1) if t > 0 else None}
+            for k, (c, t, f) in sorted(by_kind.items())}
+        for (kind, key), (cnt, tot, flop) in sorted(conv.items(), key=lambda kv: -kv[1][1])[:24]:
+            log(f"  conv {kind:16s} {key:40s} x{cnt // args.steps:<3d} {tot / args.steps:7.2f} ms/step "
+                f"{flop * cnt / (tot / 1e3) / 1e12:7.1f} TF/s")
         del trainer
         torch.cuda.empty_cache()
 

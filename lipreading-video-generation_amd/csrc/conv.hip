@@ -19,6 +19,7 @@
 // registers -> LDS (double buffered, one barrier per K step); LDS rows of
 // 64 B use a chunk XOR swizzle that is conflict-free for the fragment reads.
 #include "vd_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -408,6 +409,417 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgtGeom g, const T
     }
 }
 
+// ----------------------------------------------------------------- bf16 implicit GEMM, tap-outer
+// bf16 fwd / bwd-data.  K is walked tap-major: for each of the kt*kh*kw taps the source
+// pixel of every tile row is one add and three range checks away from a per-row base
+// computed once per workgroup (no per-step integer division), then the tap's channels
+// go in 64-wide K steps (two 16x16x32 MFMA k-slices per LDS stage, one barrier per step).
+// Tile BM x BN, 4 waves laid out WAVES_M x (4 / WAVES_M), wave tile (BM / WAVES_M) x
+// (BN * WAVES_M / 4).  LDS rows are 128 B (64 bf16); chunk c of row r sits at
+// c ^ ((r >> 1) & 7): a 16-lane group of a 16x16x32 fragment read (rows r0..r0+15, one
+// chunk) then covers all 64 banks once, and the 8-lane groups of the 16-B stores write
+// one row each.  Register-staged double buffer: the next step's global loads are in flight
+// during this step's MFMAs.
+constexpr int kIgBK = 64;
+// VDIFF_CONV_LEGACY=1: the previous k-major kernel for bf16 too (A/B measurements)
+const bool g_legacy_conv = [] {
+  const char* e = getenv("VDIFF_CONV_LEGACY");
+  return e && e[0] == '1';
+}();
+
+__device__ __forceinline__ int ig_off(int r, int c) {  // element offset of chunk c, row r
+  return r * kIgBK + ((c ^ ((r >> 1) & 7)) << 3);
+}
+
+template <int BM, int BN, int WAVES_M, bool TR>
+__global__ __launch_bounds__(kThreads, 2) void igemm_bf16_kernel(
+    GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
+    bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
+    const bf16_t* __restrict__ residual) {
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int NI = WTM / 16, NJ = WTN / 16;
+  constexpr int RA = BM / 32, RB = BN / 32;  // 16-B chunks per thread per stage
+  constexpr int A_ELEMS = BM * kIgBK, B_ELEMS = BN * kIgBK, STAGE = A_ELEMS + B_ELEMS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ch = tid & 7;   // 16-B chunk of the 64-wide K step this thread stages
+  const int rr = tid >> 3;  // first staged row (then + 32 i)
+  const int C = g.sC;
+  const int taps = g.kt * g.kh * g.kw;
+  const bool unit = g.st == 1 && g.sh == 1 && g.sw == 1;
+
+  // per staged A row: base source coordinates and the pixel index at tap (0, 0, 0)
+  int a_t[RA], a_h[RA], a_w[RA];
+  int64_t a_pix[RA];
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    int64_t m = m0 + rr + 32 * i;
+    const bool ok = m < g.M;
+    if (!ok) m = 0;
+    const int w = (int)(m % g.dW); m /= g.dW;
+    const int h = (int)(m % g.dH); m /= g.dH;
+    const int t = (int)(m % g.dT);
+    const int b = (int)(m / g.dT);
+    if (!TR) {
+      a_t[i] = t * g.st - g.pt; a_h[i] = h * g.sh - g.ph; a_w[i] = w * g.sw - g.pw;
+    } else {  // dY row of input pixel (t, h, w) at tap (a, b, c): (t + pt - a) / st, ...
+      a_t[i] = t + g.pt; a_h[i] = h + g.ph; a_w[i] = w + g.pw;
+    }
+    if (!ok) a_t[i] = -(1 << 28);  // never in range
+    a_pix[i] = (int64_t)b * g.sT * g.sH * g.sW;
+  }
+
+  auto load = [&](int tap, int c0, uint4 (&ra)[RA], uint4 (&rb)[RB]) {
+    const int ta = tap / (g.kh * g.kw), rem = tap - ta * (g.kh * g.kw);
+    const int tb = rem / g.kw, tc = rem - tb * g.kw;
+    const int c = c0 + ch * 8;
+    const bool cin = c < C;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      int st_, sh_, sw_;
+      bool ok = cin;
+      if (!TR) {
+        st_ = a_t[i] + ta; sh_ = a_h[i] + tb; sw_ = a_w[i] + tc;
+      } else if (unit) {
+        st_ = a_t[i] - ta; sh_ = a_h[i] - tb; sw_ = a_w[i] - tc;
+      } else {
+        const int nt = a_t[i] - ta, nh = a_h[i] - tb, nw = a_w[i] - tc;
+        ok = ok && nt >= 0 && nh >= 0 && nw >= 0 && nt % g.st == 0 && nh % g.sh == 0 &&
+             nw % g.sw == 0;
+        st_ = nt / g.st; sh_ = nh / g.sh; sw_ = nw / g.sw;
+      }
+      ok = ok && (unsigned)st_ < (unsigned)g.sT && (unsigned)sh_ < (unsigned)g.sH &&
+           (unsigned)sw_ < (unsigned)g.sW;
+      const int64_t pix = a_pix[i] + ((int64_t)st_ * g.sH + sh_) * g.sW + sw_;
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(src + pix * g.sCs + c) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int n = n0 + rr + 32 * i;
+      rb[i] = (n < g.N && cin)
+                  ? *reinterpret_cast<const uint4*>(wt + (int64_t)n * g.K + (int64_t)tap * C + c)
+                  : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int stage, const uint4 (&ra)[RA], const uint4 (&rb)[RB]) {
+    bf16_t* As = lds + stage * STAGE;
+    bf16_t* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) *reinterpret_cast<uint4*>(As + ig_off(rr + 32 * i, ch)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) *reinterpret_cast<uint4*>(Bs + ig_off(rr + 32 * i, ch)) = rb[i];
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int csteps = (C + kIgBK - 1) / kIgBK;
+  const int nk = taps * csteps;
+  uint4 ra[RA], rb[RB];
+  load(0, 0, ra, rb);
+  store(0, ra, rb);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  int tap = 0, cs = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (++cs == csteps) {
+      cs = 0;
+      ++tap;
+    }
+    if (more) load(tap, cs * kIgBK, ra, rb);
+    const bf16_t* As = lds + (kt & 1) * STAGE;
+    const bf16_t* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[NI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + ig_off(wm * WTM + 16 * i + fr, 4 * s + fq));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ig_off(wn * WTN + 16 * j + fr, 4 * s + fq));
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store((kt + 1) & 1, ra, rb);
+    __syncthreads();
+  }
+
+  // ---- epilogue: the fp32 tile through LDS, then coalesced 16-B stores
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int LDC = BN + 4;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WTM + 16 * i + fq * 4 + r) * LDC + wn * WTN + 16 * j + fr] = acc[i][j][r];
+  __syncthreads();
+  const int64_t pix_per_b = (int64_t)g.dT * g.dH * g.dW;
+  const bool vec = (g.N % 8 == 0) && (g.dNs % 8 == 0);
+  for (int v = tid; v < BM * BN / 8; v += kThreads) {
+    const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+    const int64_t m = m0 + r;
+    const int n = n0 + c;
+    if (m >= g.M || n >= g.N) continue;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
+    const int bidx = (int)(m / pix_per_b);
+    const int lim = g.N - n < 8 ? g.N - n : 8;
+    if (bias)
+      for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
+    if (chan_add)
+      for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)bidx * g.N + n + e];
+    bf16_t* out = dst + m * g.dNs + n;
+    if (vec) {
+      if (residual) {
+        float rv[8];
+        load8(residual + m * g.dNs + n, rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rv[e];
+      }
+      store8(out, o);
+    } else {
+      for (int e = 0; e < lim; ++e) {
+        float val = o[e];
+        if (residual) val += bf2f(residual[m * g.dNs + n + e]);
+        out[e] = f2bf(val);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, bool TR>
+void launch_ig(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
+               const float* ca, const void* res, hipStream_t st) {
+  const size_t lds_ab = 2 * (size_t)(BM + BN) * kIgBK * 2;
+  const size_t lds_c = (size_t)BM * (BN + 4) * 4;
+  const size_t lds = lds_ab > lds_c ? lds_ab : lds_c;
+  auto kern = igemm_bf16_kernel<BM, BN, WM, TR>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(g.M, BM), (unsigned)vd_cdiv(g.N, BN));
+  kern<<<grid, kThreads, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias,
+                                    ca, (const bf16_t*)res);
+}
+
+// Tile choice: N <= 64 -> 256 x 64 (4 waves along M); otherwise 128 x 128, or 64 x 128 when
+// 128 x 128 tiles would leave the chip with fewer than two workgroups per CU.
+template <bool TR>
+int launch_igemm(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
+                 const float* ca, const void* res, hipStream_t st) {
+  if (g.N <= 64) {
+    launch_ig<256, 64, 4, TR>(g, src, wt, dst, bias, ca, res, st);
+  } else if (vd_cdiv(g.M, 128) * vd_cdiv(g.N, 128) < 512) {
+    launch_ig<64, 128, 2, TR>(g, src, wt, dst, bias, ca, res, st);
+  } else {
+    launch_ig<128, 128, 2, TR>(g, src, wt, dst, bias, ca, res, st);
+  }
+  return VD_OK;
+}
+
+// ----------------------------------------------------------------- bf16 weight gradient, kw-strip
+// dW[co][tap][ci] += sum_m dY[m][co] X[src(m, tap)][ci] for stride-1 "same" 3x3(x3) convs.
+// A workgroup owns a 64 (co) x 64 (ci) tile for the three taps of one kernel row
+// (ta, tb, tc = 0..2) and a contiguous pixel range, in 64-pixel K steps.  A step's pixels
+// are R = 64 / Wc image rows of Wc = min(Wo, 64) pixels; the three taps read the SAME
+// dY tile and one X strip of Wc + 2 pixels per row, shifted by tc rows in LDS -- 3x fewer
+// operand loads than one tap per workgroup.  Both operands are read transposed from
+// [pixel][channel] LDS rows (ds_read_b64_tr_b16; each lane addresses its own row, so the
+// shifted windows cost nothing).  Pixel coordinates advance incrementally (no division in
+// the loop); the fp32 result is added into dW with atomics (split-K over pixels).
+template <int RW>  // R x (Wc + 2) strip rows, padded to a multiple of 32
+__global__ __launch_bounds__(kThreads, 2) void wgrad_bf16_kernel(
+    WgtGeom g, int wc, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+    float* __restrict__ dw) {
+  constexpr int LD = 72;              // LDS row: 64 channels + 8 pad (144 B)
+  constexpr int YROWS = 64, XROWS = RW;
+  constexpr int STAGE = (YROWS + XROWS) * LD;
+  constexpr int XCH = XROWS * 8 / kThreads;  // X chunks per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int co_tiles = (g.Co + 63) / 64, ci_tiles = (g.Ci + 63) / 64;
+  int bid = blockIdx.x;
+  const int cot = bid % co_tiles; bid /= co_tiles;
+  const int cit = bid % ci_tiles; bid /= ci_tiles;
+  const int tab = bid;                      // ta * kh + tb
+  const int ta = tab / g.kh, tb = tab % g.kh;
+  const int co0 = cot * 64, ci0 = cit * 64;
+  const int64_t mbeg = (int64_t)blockIdx.y * g.m_per_split;
+  int64_t mend = mbeg + g.m_per_split;
+  if (mend > g.M) mend = g.M;
+  if (mbeg >= mend) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid & 7, r0 = tid >> 3;
+  const int R = 64 / wc, SW = wc + 2;       // rows per step, strip width
+  // this thread's strip rows: row-in-step rr and strip column j (pixel w0 + j - 1)
+  int x_rr[XCH], x_j[XCH];
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int sr = r0 + 32 * i;
+    x_rr[i] = sr / SW;
+    x_j[i] = sr - x_rr[i] * SW;
+    if (x_rr[i] >= R) x_rr[i] = -1;  // padding row: zero
+  }
+  // coordinates of the first pixel of the current step (incremental)
+  int cb, ct, chh, cw;
+  {
+    int64_t m = mbeg;
+    cw = (int)(m % g.Wo); m /= g.Wo;
+    chh = (int)(m % g.Ho); m /= g.Ho;
+    ct = (int)(m % g.To);
+    cb = (int)(m / g.To);
+  }
+  auto advance = [&]() {  // by 64 pixels
+    cw += 64;
+    while (cw >= g.Wo) {
+      cw -= g.Wo;
+      if (++chh == g.Ho) {
+        chh = 0;
+        if (++ct == g.To) {
+          ct = 0;
+          ++cb;
+        }
+      }
+    }
+  };
+
+  auto load = [&](int64_t ms, uint4 (&ry)[2], uint4 (&rx)[XCH]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t m = ms + r0 + 32 * i;
+      ry[i] = (m < mend && co0 + ch * 8 < g.Co)
+                  ? *reinterpret_cast<const uint4*>(dy + m * g.yCs + co0 + ch * 8)
+                  : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      rx[i] = make_uint4(0, 0, 0, 0);
+      if (x_rr[i] < 0 || ci0 + ch * 8 >= g.Ci) continue;
+      // image row x_rr of this step: (cb, ct, chh + x_rr) with carry; w from cw
+      int b = cb, t = ct, h = chh + x_rr[i];
+      while (h >= g.Ho) {
+        h -= g.Ho;
+        if (++t == g.To) {
+          t = 0;
+          ++b;
+        }
+      }
+      const int ti = t - g.pt + ta, hi = h - g.ph + tb, wi = cw + x_j[i] - g.pw;
+      if (b < g.B && (unsigned)ti < (unsigned)g.Ti && (unsigned)hi < (unsigned)g.Hi &&
+          (unsigned)wi < (unsigned)g.Wi) {
+        const int64_t pix = (((int64_t)b * g.Ti + ti) * g.Hi + hi) * g.Wi + wi;
+        rx[i] = *reinterpret_cast<const uint4*>(x + pix * g.xCs + ci0 + ch * 8);
+      }
+    }
+  };
+  auto store = [&](int stage, const uint4 (&ry)[2], const uint4 (&rx)[XCH]) {
+    bf16_t* Ys = lds + stage * STAGE;
+    bf16_t* Xs = Ys + YROWS * LD;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(Ys + (r0 + 32 * i) * LD + ch * 8) = ry[i];
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) *reinterpret_cast<uint4*>(Xs + (r0 + 32 * i) * LD + ch * 8) = rx[i];
+  };
+
+  // wave tile: co [32 wm, +32) x ci [32 wn, +32) x 3 taps
+  const int wm = wave & 1, wn = wave >> 1;
+  f32x4 acc[3][2][2];
+#pragma unroll
+  for (int tc = 0; tc < 3; ++tc)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[tc][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (int)((mend - mbeg + 63) / 64);
+  uint4 ry[2], rx[XCH];
+  load(mbeg, ry, rx);
+  store(0, ry, rx);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4, q4 = fr >> 2, p4 = fr & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps;
+    if (more) {
+      advance();
+      load(mbeg + (int64_t)(s + 1) * 64, ry, rx);
+    }
+    const bf16_t* Ys = lds + (s & 1) * STAGE;
+    const bf16_t* Xs = Ys + YROWS * LD;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // lane group fq covers pixels p = 32 ks + 8 fq + (0..7); block row q4 (+4)
+      const int p_lo = 32 * ks + 8 * fq + q4, p_hi = p_lo + 4;
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c0 = wm * 32 + 16 * i + 4 * p4;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Ys + p_lo * LD + c0));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Ys + p_hi * LD + c0));
+        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      // strip row of pixel p at tap tc: (p / wc) * (wc + 2) + p % wc + tc
+      const int s_lo = (p_lo / wc) * SW + p_lo % wc, s_hi = (p_hi / wc) * SW + p_hi % wc;
+#pragma unroll
+      for (int tc = 0; tc < 3; ++tc) {
+        bf16x8 bfr[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c0 = wn * 32 + 16 * j + 4 * p4;
+          const bf16x4 lo =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Xs + (s_lo + tc) * LD + c0));
+          const bf16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Xs + (s_hi + tc) * LD + c0));
+          bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[tc][i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[tc][i][j], 0, 0, 0);
+      }
+    }
+    if (more) store((s + 1) & 1, ry, rx);
+    __syncthreads();
+  }
+  const int taps = g.kt * g.kh * g.kw;
+  const int64_t krow = (int64_t)taps * g.Ci;
+#pragma unroll
+  for (int tc = 0; tc < 3; ++tc) {
+    const int tap = tab * g.kw + tc;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = ci0 + wn * 32 + 16 * j + fr;
+        if (ci >= g.Ci) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wm * 32 + 16 * i + fq * 4 + r;
+          if (co < g.Co) atomicAdd(dw + (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
+        }
+      }
+  }
+}
+
 int check_desc(const vd_conv_desc* d) {
   VD_REQUIRE(d, "null descriptor");
   VD_REQUIRE(d->B > 0 && d->Ti > 0 && d->Hi > 0 && d->Wi > 0 && d->Ci > 0 && d->To > 0 &&
@@ -430,6 +842,9 @@ int check_desc(const vd_conv_desc* d) {
 template <typename T, bool TR>
 int launch_gemm(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
                 const float* ca, const void* res, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (!g_legacy_conv) return launch_igemm<TR>(g, src, wt, dst, bias, ca, res, st);
+  }
   const int64_t mt = vd_cdiv(g.M, 128);
   const bool narrow = g.N <= 64;
   if (narrow) {
@@ -515,6 +930,33 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
   g.pt = d->pt; g.ph = d->ph; g.pw = d->pw;
   g.M = (int64_t)d->B * d->To * d->Ho * d->Wo;
   const int taps = d->kt * d->kh * d->kw;
+  // bf16 stride-1 "same" 3x3(x3) convs with image rows that tile into 64-pixel steps:
+  // the kw-strip kernel (three taps per workgroup)
+  const bool strip = d->dtype == VD_BF16 && !g_legacy_conv && d->kh == 3 && d->kw == 3 &&
+                     (d->kt == 1 || d->kt == 3) && d->st == 1 && d->sh == 1 && d->sw == 1 &&
+                     d->pt == d->kt / 2 && d->ph == 1 && d->pw == 1 &&
+                     (d->Wo % 64 == 0 || (64 % d->Wo == 0 && 64 / d->Wo <= d->Ho));
+  if (strip) {
+    const int wc = d->Wo < 64 ? d->Wo : 64;
+    const int rows = (64 / wc) * (wc + 2);
+    const int64_t tiles = (int64_t)vd_cdiv(d->Co, 64) * vd_cdiv(d->Ci, 64) * d->kt * d->kh;
+    int64_t splits = vd_cdiv(2048, tiles);
+    int64_t maxs = vd_cdiv(g.M, 1024);
+    if (splits > maxs) splits = maxs;
+    if (splits < 1) splits = 1;
+    g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
+    splits = vd_cdiv(g.M, g.m_per_split);
+    dim3 grid((unsigned)tiles, (unsigned)splits);
+    hipStream_t st = VD_STREAM(stream);
+#define VD_WG(RW)                                                                        \
+  wgrad_bf16_kernel<RW><<<grid, kThreads, 2 * (64 + RW) * 72 * 2, st>>>(                \
+      g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw)
+    if (rows <= 96) VD_WG(96);
+    else if (rows <= 128) VD_WG(128);
+    else VD_WG(192);
+#undef VD_WG
+    return vd::check_launch("conv_wgrad");
+  }
   const int64_t tiles = (int64_t)vd_cdiv(d->Co, 64) * vd_cdiv(d->Ci, 64) * taps;
   // split the pixel reduction so the grid has ~2048 workgroups, >= 512 px each
   int64_t splits = vd_cdiv(2048, tiles);

@@ -356,6 +356,15 @@ def _pad_channels(x: torch.Tensor, cpad: int) -> torch.Tensor:
     return phys.movedim(-1, 1)
 
 
+def _conv_key(Ci, Co, k, s, out):
+    return f"{Ci}->{Co} k{'x'.join(map(str, k))} s{'x'.join(map(str, s))} out{'x'.join(map(str, out))}"
+
+
+def _conv_flop(B, out, Co, k, Ci):
+    """Algorithmic FLOP of one conv product (2 per MAC, unpadded channels)."""
+    return 2.0 * B * out[0] * out[1] * out[2] * Co * k[0] * k[1] * k[2] * Ci
+
+
 class ConvFn(torch.autograd.Function):
     """y = conv(x, w) + bias + chan_add[b, co] + residual, channels-last, implicit GEMM."""
 
@@ -385,8 +394,12 @@ class ConvFn(torch.autograd.Function):
             if list(res.shape) != ys:
                 raise ValueError(f"residual shape {list(res.shape)} != output {ys}")
         d = _desc(B, sp, Cip, out, Co, k, s, p, _DT[dt])
+        ev = _timer.begin() if _timer is not None else None
         _lib.call("vd_conv3d_fwd", d, _p(xp), _p(w_fwd), _p(b32), _p(ca), _p(res), _p(y),
                   _stream(x))
+        if ev is not None:
+            _timer.end_conv(ev, "conv_fwd", _conv_key(Cip, Co, k, s, out),
+                            _conv_flop(B, out, Co, k, Ci))
         ctx.save_for_backward(xp, weight)
         ctx.cfg = (k, s, p, sp, out, B, Ci, Cip, Co, nd, list(x.shape), bias is not None,
                    chan_add is not None, residual is not None,
@@ -415,11 +428,19 @@ class ConvFn(torch.autograd.Function):
             w_bwd = torch.zeros(Cip, taps, Cop, dtype=dt, device=dy.device)
             w_bwd[:Ci, :, :Co] = w.permute(1, 2, 0)
             dxp = empty_cl([B, Cip] + xshape[2:], dt, dy.device)
+            ev = _timer.begin() if _timer is not None else None
             _lib.call("vd_conv3d_bwd_data", d, _p(dyp), _p(w_bwd), _p(dxp), st)
+            if ev is not None:
+                _timer.end_conv(ev, "conv_bwd_data", _conv_key(Cip, Co, k, s, out),
+                                _conv_flop(B, out, Co, k, Ci))
             dx = dxp[:, :Ci] if Cip != Ci else dxp
         if ctx.needs_input_grad[1]:
             dwp = torch.zeros(Cop, taps, Cip, dtype=torch.float32, device=dy.device)
+            ev = _timer.begin() if _timer is not None else None
             _lib.call("vd_conv3d_bwd_weight", d, _p(xp), _p(dyp), _p(dwp), st)
+            if ev is not None:
+                _timer.end_conv(ev, "conv_bwd_weight", _conv_key(Cip, Co, k, s, out),
+                                _conv_flop(B, out, Co, k, Ci))
             dw = dwp[:Co, :, :Ci].permute(0, 2, 1).reshape(weight.shape).to(weight.dtype)
         red = [0] + list(range(2, dy.dim()))
         if has_b and ctx.needs_input_grad[2]:
@@ -449,6 +470,7 @@ class KernelTimer:
 
     def __init__(self):
         self.records = []
+        self.conv_records = []  # (kind, geometry key, flop, start, end): implicit-GEMM convs
 
     def begin(self):
         e = torch.cuda.Event(enable_timing=True)
@@ -459,6 +481,21 @@ class KernelTimer:
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         self.records.append((kind, d.head_dim, d.seq_len, d.nseq, start, e))
+
+    def end_conv(self, start, kind, key, flop):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.conv_records.append((kind, key, flop, start, e))
+
+    def conv_summary(self):
+        """{(kind, key): [count, total_ms, flop per launch]} (synchronizes)."""
+        torch.cuda.synchronize()
+        out = {}
+        for kind, key, flop, s, e in self.conv_records:
+            c = out.setdefault((kind, key), [0, 0.0, flop])
+            c[0] += 1
+            c[1] += s.elapsed_time(e)
+        return out
 
     def summary(self):
         """{(kind, head_dim, seq_len, nseq): [count, total_ms]} (synchronizes)."""

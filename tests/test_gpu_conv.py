@@ -20,6 +20,12 @@ CASES = [
     ((2, 64, 200), 192, 1, 1, 0),              # AttentionBlock qkv (Conv1d)
     ((2, 64, 10, 10), 64, 3, 1, 1),            # dims = 2
     ((1, 32, 4, 16, 16), 32, 3, 1, 1),
+    ((1, 64, 2, 16, 24), 64, 3, 1, 1),         # bf16 tap-outer kernel: 256 x 64 tiles, ragged M
+    ((1, 128, 3, 12, 12), 256, 3, 1, 1),       # 64 x 128 tiles (few workgroups)
+    ((1, 128, 4, 128, 128), 128, 1, 1, 0),     # 128 x 128 tiles
+    ((1, 128, 3, 10, 10), 128, 3, (1, 2, 2), 1),  # strided: transposed gather with stride 2
+    ((2, 64, 3, 4, 32), 64, 3, 1, 1),          # bf16 kw-strip wgrad: 2 rows / step, t and b carry
+    ((1, 64, 2, 3, 64), 128, 3, 1, 1),         # kw-strip wgrad: one 64-pixel row / step
 ]
 
 
