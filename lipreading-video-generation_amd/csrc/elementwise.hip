@@ -250,6 +250,74 @@ __global__ void upsample_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx
 
 }  // namespace
 
+
+// ---------------------------------------------------------------- conv glue
+// Per-(sample, channel) sums of a channels-last activation: the bias gradient and the
+// ResBlock emb-add (chan_add) gradient of a conv in one pass over dY (reference autograd of
+// conv_nd's bias, utils.py:59-69, and of `h + emb_out` at unet.py:255-258).  A block owns a
+// run of rows of one sample; each thread sums 8 channels over its rows in fp32, the block
+// reduces through LDS and adds into out[b][c] (zeroed by the launcher).
+template <typename T>
+__global__ __launch_bounds__(256) void channel_sums_kernel(const T* __restrict__ x, int64_t S,
+                                                           int C, int cs, int64_t rows_per_blk,
+                                                           float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int b = blockIdx.y;
+  const int tpr = C / 8;                 // threads per row (C <= 2048)
+  const int rpi = 256 / tpr;             // rows per iteration
+  const int tid = threadIdx.x;
+  const int lr = tid / tpr, c8 = (tid % tpr) * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  int64_t r1 = r0 + rows_per_blk;
+  if (r1 > S) r1 = S;
+  if (lr < rpi) {
+    const T* base = x + (int64_t)b * S * cs + c8;
+    for (int64_t r = r0 + lr; r < r1; r += rpi) {
+      float v[8];
+      load8(base + r * cs, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = acc[e];
+  __syncthreads();
+  // thread (lr = 0, channel group g) sums the rpi rows of its channel group
+  if (tid < tpr) {
+    float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < rpi; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s8[e] += red[(k * tpr + tid) * 8 + e];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(out + (int64_t)b * C + tid * 8 + e, s8[e]);
+  }
+}
+
+// fp32 torch weight [Co][Ci][taps] -> packed operand in the activation dtype, channels
+// zero-padded: fwd  [Co][taps][Cip]  (transpose = 0)
+//              bwd  [Cip][taps][Cop] (transpose = 1, the transposed-conv operand)
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ w, int Co, int Ci, int taps, int Cip,
+                                   int Cop, int transpose, T* __restrict__ out) {
+  const int64_t total = transpose ? (int64_t)Cip * taps * Cop : (int64_t)Co * taps * Cip;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int co, ci, tap;
+    if (!transpose) {
+      ci = (int)(i % Cip);
+      tap = (int)((i / Cip) % taps);
+      co = (int)(i / ((int64_t)Cip * taps));
+    } else {
+      co = (int)(i % Cop);
+      tap = (int)((i / Cop) % taps);
+      ci = (int)(i / ((int64_t)Cop * taps));
+    }
+    const float v = (co < Co && ci < Ci) ? w[((int64_t)co * Ci + ci) * taps + tap] : 0.f;
+    Elem<T>::st(out + i, v);
+  }
+}
+
 extern "C" {
 
 int vd_timestep_embedding(const int64_t* t, int B, int dim, float max_period, float* out,
@@ -348,6 +416,40 @@ int vd_upsample_nearest_hw_bwd(const void* dy, void* dx, int B, int T, int H, in
     else
       upsample_bwd_kernel<Tp, 1><<<grid_for(work), kBlock, 0, VD_STREAM(stream)>>>(
           (const Tp*)dy, (Tp*)dx, BT, H, W, C);
+  });
+}
+
+int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dtype, float* out,
+                    void* stream) {
+  VD_REQUIRE(x && out, "null argument");
+  VD_REQUIRE(B > 0 && S > 0 && C > 0 && C % 8 == 0 && C <= 2048, "bad shape B=%d C=%d", B, C);
+  const int cs = cstride ? cstride : C;
+  VD_REQUIRE(cs >= C && cs % 8 == 0, "bad channel stride %d", cs);
+  hipStream_t st = VD_STREAM(stream);
+  if (hipMemsetAsync(out, 0, (size_t)B * C * sizeof(float), st) != hipSuccess)
+    return vd::fail(VD_ELAUNCH, "memset");
+  // ~4 blocks per CU over the whole batch
+  int64_t blocks = vd_cdiv(1024, B);
+  const int64_t rpi = 256 / (C / 8);
+  int64_t maxb = vd_cdiv(S, rpi * 4);
+  if (blocks > maxb) blocks = maxb;
+  if (blocks < 1) blocks = 1;
+  const int64_t rows = vd_cdiv(S, blocks);
+  blocks = vd_cdiv(S, rows);
+  return VD_DISPATCH_DTYPE(dtype, Tp, {
+    channel_sums_kernel<Tp><<<dim3((unsigned)blocks, (unsigned)B), 256, 0, st>>>(
+        (const Tp*)x, S, C, cs, rows, out);
+  });
+}
+
+int vd_conv_pack_weight(const float* w, int Co, int Ci, int taps, int Cip, int Cop, int transpose,
+                        int dtype, void* out, void* stream) {
+  VD_REQUIRE(w && out, "null argument");
+  VD_REQUIRE(Co > 0 && Ci > 0 && taps > 0 && Cip >= Ci && Cop >= Co, "bad weight shape");
+  const int64_t total = transpose ? (int64_t)Cip * taps * Cop : (int64_t)Co * taps * Cip;
+  return VD_DISPATCH_DTYPE(dtype, Tp, {
+    pack_weight_kernel<Tp><<<grid_for(total), kBlock, 0, VD_STREAM(stream)>>>(
+        w, Co, Ci, taps, Cip, Cop, transpose, (Tp*)out);
   });
 }
 

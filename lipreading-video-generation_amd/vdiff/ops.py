@@ -356,6 +356,33 @@ def _pad_channels(x: torch.Tensor, cpad: int) -> torch.Tensor:
     return phys.movedim(-1, 1)
 
 
+def _pack_weight(weight, Co, Ci, taps, Cip, Cop, transpose, dt):
+    """torch [Co][Ci][*k] weight -> packed fwd [Co][taps][Cip] / bwd [Cip][taps][Cop] operand."""
+    w = weight.detach()
+    if w.dtype != torch.float32:
+        w = w.float()
+    w = w.contiguous()
+    shape = (Cip, taps, Cop) if transpose else (Co, taps, Cip)
+    out = torch.empty(shape, dtype=dt, device=w.device)
+    _lib.call("vd_conv_pack_weight", _p(w), Co, Ci, taps, Cip, Cop, int(transpose), _DT[dt],
+              _p(out), _stream(w))
+    return out
+
+
+def channel_sums(x: torch.Tensor) -> torch.Tensor:
+    """[B, C, *spatial] channels-last -> fp32 [B, C] sums over the spatial dims."""
+    _gpu(x)
+    x = to_cl(x)
+    B, Cc = x.shape[0], x.shape[1]
+    S = _spatial(x)
+    if Cc % 8:
+        x = _pad_channels(x, (Cc + 7) // 8 * 8)
+    cp = x.shape[1]
+    out = torch.empty(B, cp, dtype=torch.float32, device=x.device)
+    _lib.call("vd_channel_sums", _p(x), B, S, cp, 0, _dtype(x), _p(out), _stream(x))
+    return out[:, :Cc]
+
+
 def _conv_key(Ci, Co, k, s, out):
     return f"{Ci}->{Co} k{'x'.join(map(str, k))} s{'x'.join(map(str, s))} out{'x'.join(map(str, out))}"
 
@@ -381,9 +408,7 @@ class ConvFn(torch.autograd.Function):
         taps = k[0] * k[1] * k[2]
         Cip = (Ci + 7) // 8 * 8
         xp = _pad_channels(x, Cip)
-        w = weight.detach().reshape(Co, Ci, taps).to(dt)
-        w_fwd = torch.zeros(Co, taps, Cip, dtype=dt, device=x.device)
-        w_fwd[:, :, :Ci] = w.permute(0, 2, 1)
+        w_fwd = _pack_weight(weight, Co, Ci, taps, Cip, Co, False, dt)
         ys = [B, Co] + out[3 - nd:] if nd > 0 else [B, Co]
         y = empty_cl(ys, dt, x.device)
         b32 = None if bias is None else bias.detach().float().contiguous()
@@ -424,9 +449,7 @@ class ConvFn(torch.autograd.Function):
         if Cop != Co:
             d = _desc(B, sp, Cip, out, Cop, k, s, p, _DT[dt])
         if ctx.needs_input_grad[0]:
-            w = weight.detach().reshape(Co, Ci, taps).to(dt)
-            w_bwd = torch.zeros(Cip, taps, Cop, dtype=dt, device=dy.device)
-            w_bwd[:Ci, :, :Co] = w.permute(1, 2, 0)
+            w_bwd = _pack_weight(weight, Co, Ci, taps, Cip, Cop, True, dt)
             dxp = empty_cl([B, Cip] + xshape[2:], dt, dy.device)
             ev = _timer.begin() if _timer is not None else None
             _lib.call("vd_conv3d_bwd_data", d, _p(dyp), _p(w_bwd), _p(dxp), st)
@@ -442,11 +465,14 @@ class ConvFn(torch.autograd.Function):
                 _timer.end_conv(ev, "conv_bwd_weight", _conv_key(Cip, Co, k, s, out),
                                 _conv_flop(B, out, Co, k, Ci))
             dw = dwp[:Co, :, :Ci].permute(0, 2, 1).reshape(weight.shape).to(weight.dtype)
-        red = [0] + list(range(2, dy.dim()))
-        if has_b and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=red).to(bdt)
-        if has_ca and ctx.needs_input_grad[3]:
-            dca = dy.float().sum(dim=list(range(2, dy.dim()))).reshape(ca_shape)
+        want_b = has_b and ctx.needs_input_grad[2]
+        want_ca = has_ca and ctx.needs_input_grad[3]
+        if want_b or want_ca:
+            sums = channel_sums(dyp)[:, :Co]  # [B, Co] fp32: one pass over dY for both
+            if want_b:
+                db = sums.sum(0).to(bdt)
+            if want_ca:
+                dca = sums.reshape(ca_shape)
         if has_res and ctx.needs_input_grad[4]:
             dres = dy
         return dx, dw, db, dca, dres, None, None

@@ -5,7 +5,7 @@ import torch
 
 from oracle import nn as onn
 from oracle import schedulers as osch
-from oracle.fixtures import seeded
+from oracle.fixtures import rel_l2, seeded
 
 from conftest import golden
 
@@ -122,3 +122,33 @@ def test_upsample_fwd_bwd(dtype, C):
     onn.upsample(xr, 3).backward(g)
     tol = 1e-6 if dtype == torch.float32 else 3e-2
     torch.testing.assert_close(xd.grad.float().cpu(), xr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 3, 5, 7), (1, 256, 4, 4, 4), (3, 3, 2, 2, 2),
+                                   (2, 72, 1000)])
+def test_channel_sums(shape, dtype):
+    """vd_channel_sums (conv bias / chan_add gradients) vs a torch fp32 reduction."""
+    from vdiff import ops
+    x = seeded(shape, 70)
+    ref = x.to(dtype).float().sum(dim=list(range(2, x.dim())))
+    got = ops.channel_sums(ops.to_cl(x.to(dev, dtype)))
+    assert got.shape == ref.shape
+    assert rel_l2(got, ref) < 1e-5
+
+
+@pytest.mark.parametrize("transpose", [False, True])
+def test_conv_pack_weight(transpose):
+    from vdiff import ops
+    Co, Ci, taps = 20, 13, 27
+    w = seeded((Co, Ci, 3, 3, 3), 71)
+    Cip, Cop = 16, 24
+    got = ops._pack_weight(w.to(dev), Co, Ci, taps, Cip, Cop, transpose, torch.bfloat16).float()
+    wr = w.reshape(Co, Ci, taps).bfloat16().float()
+    if transpose:
+        ref = torch.zeros(Cip, taps, Cop)
+        ref[:Ci, :, :Co] = wr.permute(1, 2, 0)
+    else:
+        ref = torch.zeros(Co, taps, Cip)
+        ref[:, :, :Ci] = wr.permute(0, 2, 1)
+    assert torch.equal(got.cpu(), ref)
