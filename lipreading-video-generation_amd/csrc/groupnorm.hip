@@ -153,32 +153,42 @@ __global__ __launch_bounds__(kThreads) void gn_finalize_kernel(const float* __re
   }
 }
 
+// grid (nchunk, B): each thread keeps one 8-channel vector for all its pixel rows, so the
+// per-channel scale/shift (gamma * rstd, beta - mean * gamma * rstd) is computed once and
+// the loop is one FMA (+ SiLU, dropout) per element -- no index division per element.
 template <typename T, bool SILU>
 __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict__ x,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
-                                                            T* __restrict__ y, int B, int64_t S,
-                                                            int C, int G, Drop drop) {
-  const int nvec = C / kVec;
-  const int cpg = C / G;
-  const int64_t n = (int64_t)B * S * nvec;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % nvec) * kVec;
-    const int b = (int)(i / ((int64_t)S * nvec));
+                                                            T* __restrict__ y, int64_t S, int C,
+                                                            int G, int64_t chunk_px,
+                                                            int rows_per_iter, Drop drop) {
+  const int nvec = C / kVec, cpg = C / G;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int r = tid / nvec, cv = tid % nvec;
+  if (r >= rows_per_iter) return;
+  float sc[kVec], sh[kVec];
+#pragma unroll
+  for (int j = 0; j < kVec; ++j) {
+    const int c = cv * kVec + j, g = b * G + c / cpg;
+    sc[j] = gamma[c] * rstd[g];
+    sh[j] = beta[c] - mean[g] * sc[j];
+  }
+  const int64_t p0 = (int64_t)blockIdx.x * chunk_px;
+  int64_t p1 = p0 + chunk_px;
+  if (p1 > S) p1 = S;
+  for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
+    const int64_t e0 = ((int64_t)b * S + p) * C + cv * kVec;
     float v[kVec];
-    load8(x + i * kVec, v);
+    load8(x + e0, v);
 #pragma unroll
     for (int j = 0; j < kVec; ++j) {
-      const int c = c0 + j;
-      const int g = b * G + c / cpg;
-      const float sc = gamma[c] * rstd[g];
-      const float z = (v[j] - mean[g]) * sc + beta[c];
-      v[j] = (SILU ? silu_f(z) : z) * drop.mul(i * kVec + j);
+      const float z = v[j] * sc[j] + sh[j];
+      v[j] = (SILU ? silu_f(z) : z) * drop.mul(e0 + j);
     }
-    store8(y + i * kVec, v);
+    store8(y + e0, v);
   }
 }
 
@@ -249,14 +259,19 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
 // grid (ceil(C/64), B), 1024 threads = 64 channels x 16 chunk lanes: per-(b, c) sums of
 // the chunk partials -> sums[b][c][2] (coalesced 512-B rows, 16-way parallel over chunks)
 __global__ __launch_bounds__(1024) void gn_bwd_sum_kernel(const float* __restrict__ part,
-                                                          int nchunk, int C,
+                                                          int nchunk, int C, int kper,
                                                           float* __restrict__ sums) {
+  // grid (C / 64, B, splits): this WG sums chunks [z * kper, (z + 1) * kper) and adds into
+  // sums (zeroed by the launcher) -- enough workgroups to stream the partials at speed
   __shared__ float2 sh[16][64];
   const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
+  const int k0 = blockIdx.z * kper;
+  int k1 = k0 + kper;
+  if (k1 > nchunk) k1 = nchunk;
   float2 a = make_float2(0.f, 0.f);
   if (c < C) {
-    for (int k = kl; k < nchunk; k += 16) {
+    for (int k = k0 + kl; k < k1; k += 16) {
       const float2 v = *reinterpret_cast<const float2*>(part + (((int64_t)b * nchunk + k) * C + c) * 2);
       a.x += v.x;
       a.y += v.y;
@@ -269,7 +284,8 @@ __global__ __launch_bounds__(1024) void gn_bwd_sum_kernel(const float* __restric
       a.x += sh[k][cl].x;
       a.y += sh[k][cl].y;
     }
-    *reinterpret_cast<float2*>(sums + ((int64_t)b * C + c) * 2) = a;
+    atomicAdd(sums + ((int64_t)b * C + c) * 2, a.x);
+    atomicAdd(sums + ((int64_t)b * C + c) * 2 + 1, a.y);
   }
 }
 
@@ -302,44 +318,51 @@ __global__ void gn_bwd_finalize_kernel(const float* __restrict__ sums, int B, in
   }
 }
 
+// grid (nchunk, B), per-thread channel constants as gn_apply_kernel
 template <typename T, bool SILU>
 __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
-    const float* __restrict__ coef, T* __restrict__ dx, int B, int64_t S, int C, int G,
-    Drop drop) {
-  const int nvec = C / kVec;
-  const int cpg = C / G;
-  const int64_t n = (int64_t)B * S * nvec;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % nvec) * kVec;
-    const int b = (int)(i / ((int64_t)S * nvec));
+    const float* __restrict__ coef, T* __restrict__ dx, int64_t S, int C, int G, int64_t chunk_px,
+    int rows_per_iter, Drop drop) {
+  const int nvec = C / kVec, cpg = C / G;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int r = tid / nvec, cv = tid % nvec;
+  if (r >= rows_per_iter) return;
+  float mu[kVec], rs[kVec], ga[kVec], be[kVec], c0[kVec], c1[kVec];
+#pragma unroll
+  for (int j = 0; j < kVec; ++j) {
+    const int c = cv * kVec + j, g = b * G + c / cpg;
+    mu[j] = mean[g];
+    rs[j] = rstd[g];
+    ga[j] = gamma[c];
+    be[j] = beta[c];
+    c0[j] = coef[2 * g];
+    c1[j] = coef[2 * g + 1];
+  }
+  const int64_t p0 = (int64_t)blockIdx.x * chunk_px;
+  int64_t p1 = p0 + chunk_px;
+  if (p1 > S) p1 = S;
+  for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
+    const int64_t e0 = ((int64_t)b * S + p) * C + cv * kVec;
     float v[kVec], d[kVec];
-    load8(x + i * kVec, v);
-    load8(dy + i * kVec, d);
+    load8(x + e0, v);
+    load8(dy + e0, d);
 #pragma unroll
     for (int j = 0; j < kVec; ++j) {
-      const int c = c0 + j;
-      const int g = b * G + c / cpg;
-      const float rs = rstd[g];
-      const float xh = (v[j] - mean[g]) * rs;
-      float dz = d[j] * drop.mul(i * kVec + j);
+      const float xh = (v[j] - mu[j]) * rs[j];
+      float dz = d[j] * drop.mul(e0 + j);
       if (SILU) {
-        const float z = xh * gamma[c] + beta[c];
+        const float z = xh * ga[j] + be[j];
         const float sg = 1.f / (1.f + __expf(-z));
         dz *= sg * (1.f + z * (1.f - sg));
       }
-      v[j] = rs * (gamma[c] * dz - coef[2 * g] - xh * coef[2 * g + 1]);
+      v[j] = rs[j] * (ga[j] * dz - c0[j] - xh * c1[j]);
     }
-    store8(dx + i * kVec, v);
+    store8(dx + e0, v);
   }
 }
 
-inline int apply_grid(int64_t nvec_total) {
-  int64_t g = vd_cdiv(nvec_total, kThreads);
-  return (int)(g < 256 * 16 ? (g > 0 ? g : 1) : 256 * 16);
-}
 
 int gn_check(const void* x, int B, int64_t S, int C, int G) {
   VD_REQUIRE(x, "null tensor");
@@ -384,13 +407,15 @@ int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, 
     gn_stats_kernel<T><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
         (const T*)x, S, C, G, p.chunk_px, p.rows_per_iter, part);
     gn_finalize_kernel<<<dim3(G, B), kThreads, 0, st>>>(part, p.nchunk, G, eps, mean, rstd);
-    const int grid = apply_grid((int64_t)B * S * (C / kVec));
+    const dim3 grid(p.nchunk, B);
     if (silu)
       gn_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
-                                                          (T*)y, B, S, C, G, drop);
+                                                          (T*)y, S, C, G, p.chunk_px,
+                                                          p.rows_per_iter, drop);
     else
       gn_apply_kernel<T, false><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
-                                                           (T*)y, B, S, C, G, drop);
+                                                           (T*)y, S, C, G, p.chunk_px,
+                                                           p.rows_per_iter, drop);
   });
 }
 
@@ -410,7 +435,7 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
   float* sums = coef + (size_t)B * G * 2;
   hipStream_t st = VD_STREAM(stream);
   const size_t lds = (size_t)p.rows_per_iter * C * sizeof(float2);
-  const int grid = apply_grid((int64_t)B * S * (C / kVec));
+  const dim3 grid(p.nchunk, B);
   return VD_DISPATCH_DTYPE(dtype, T, {
     if (silu)
       gn_bwd_reduce_kernel<T, true><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
@@ -420,17 +445,19 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
       gn_bwd_reduce_kernel<T, false><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
           p.rows_per_iter, part, drop);
-    gn_bwd_sum_kernel<<<dim3((unsigned)vd_cdiv(C, 64), B), 1024, 0, st>>>(part, p.nchunk, C,
-                                                                          sums);
+    (void)hipMemsetAsync(sums, 0, (size_t)B * C * 2 * sizeof(float), st);
+    const int kper = 64, ksplit = (int)vd_cdiv(p.nchunk, kper);
+    gn_bwd_sum_kernel<<<dim3((unsigned)vd_cdiv(C, 64), B, ksplit), 1024, 0, st>>>(
+        part, p.nchunk, C, kper, sums);
     gn_bwd_finalize_kernel<<<1, kThreads, 0, st>>>(sums, B, C, G, S, gamma, coef, dgamma, dbeta);
     if (silu)
-      gn_bwd_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, (const T*)dy, gamma,
-                                                              beta, mean, rstd, coef, (T*)dx, B,
-                                                              S, C, G, drop);
+      gn_bwd_apply_kernel<T, true><<<grid, kThreads, 0, st>>>(
+          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,
+          p.rows_per_iter, drop);
     else
-      gn_bwd_apply_kernel<T, false><<<grid, kThreads, 0, st>>>((const T*)x, (const T*)dy, gamma,
-                                                               beta, mean, rstd, coef, (T*)dx,
-                                                               B, S, C, G, drop);
+      gn_bwd_apply_kernel<T, false><<<grid, kThreads, 0, st>>>(
+          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,
+          p.rows_per_iter, drop);
   });
 }
 
