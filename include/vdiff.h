@@ -189,13 +189,15 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy,
 
 /* ---- Conv glue ---------------------------------------------------------
  * vd_channel_sums: out[b][c] = sum over the S pixels of x[b][s][c] (fp32; x channels-last
- * with pixel stride cstride, 0 = C; C % 8 == 0).  One pass gives both the conv bias
+ * with pixel stride cstride, 0 = C; C % 8 == 0; deterministic two-stage reduction through
+ * a caller workspace of vd_channel_sums_workspace_size bytes).  One pass gives both the conv bias
  * gradient (sum over b) and the chan_add gradient of the ResBlock emb-add -- the autograd
  * of conv_nd's bias (utils.py:59-69) and of `h = h + emb_out` (unet.py:255-258).
  * vd_conv_pack_weight: torch fp32 weight [Co][Ci][taps] -> the w_fwd [Co][taps][Cip]
  * (transpose 0) or w_bwd [Cip][taps][Cop] (transpose 1) operand above, zero-padded. */
+size_t vd_channel_sums_workspace_size(int B, int C);
 int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dtype,
-                    float* out, void* stream);
+                    float* out, void* workspace, void* stream);
 int vd_conv_pack_weight(const float* w, int Co, int Ci, int taps, int Cip, int Cop,
                         int transpose, int dtype, void* out, void* stream);
 

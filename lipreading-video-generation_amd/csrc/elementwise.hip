@@ -254,13 +254,16 @@ __global__ void upsample_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx
 // ---------------------------------------------------------------- conv glue
 // Per-(sample, channel) sums of a channels-last activation: the bias gradient and the
 // ResBlock emb-add (chan_add) gradient of a conv in one pass over dY (reference autograd of
-// conv_nd's bias, utils.py:59-69, and of `h + emb_out` at unet.py:255-258).  A block owns a
-// run of rows of one sample; each thread sums 8 channels over its rows in fp32, the block
-// reduces through LDS and adds into out[b][c] (zeroed by the launcher).
+// conv_nd's bias, utils.py:59-69, and of `h + emb_out` at unet.py:255-258).  Stage 1: a
+// block owns a run of rows of one sample, each thread sums 8 channels over its rows in fp32,
+// the block reduces through LDS and stores its partial row part[b][blk][C].  Stage 2 sums
+// the partial rows per channel (deterministic; no same-address atomics, which serialise).
+constexpr int kSumBlocks = 256;  // stage-1 blocks per sample (max)
+
 template <typename T>
 __global__ __launch_bounds__(256) void channel_sums_kernel(const T* __restrict__ x, int64_t S,
                                                            int C, int cs, int64_t rows_per_blk,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ part) {
   __shared__ float red[256 * 8];
   const int b = blockIdx.y;
   const int tpr = C / 8;                 // threads per row (C <= 2048)
@@ -283,14 +286,34 @@ __global__ __launch_bounds__(256) void channel_sums_kernel(const T* __restrict__
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[tid * 8 + e] = acc[e];
   __syncthreads();
-  // thread (lr = 0, channel group g) sums the rpi rows of its channel group
-  if (tid < tpr) {
-    float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < rpi; ++k)
+  // thread t < C sums channel t over the rpi row lanes
+  float* dst = part + ((int64_t)b * gridDim.x + blockIdx.x) * C;
+  for (int c = tid; c < C; c += 256) {
+    const int g = c / 8, e = c % 8;
+    float sum = 0.f;
+    for (int k = 0; k < rpi; ++k) sum += red[(k * tpr + g) * 8 + e];
+    dst[c] = sum;
+  }
+}
+
+// 32 channels per block, 8 row lanes per channel (independent loads in flight), LDS reduce
+__global__ __launch_bounds__(256) void channel_sums_finish_kernel(const float* __restrict__ part,
+                                                                  int nblk, int C,
+                                                                  float* __restrict__ out) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, kl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl, b = blockIdx.y;
+  float sum = 0.f;
+  if (c < C) {
+    const float* p = part + (int64_t)b * nblk * C + c;
+    for (int k = kl; k < nblk; k += 8) sum += p[(int64_t)k * C];
+  }
+  red[kl][cl] = sum;
+  __syncthreads();
+  if (kl == 0 && c < C) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s8[e] += red[(k * tpr + tid) * 8 + e];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(out + (int64_t)b * C + tid * 8 + e, s8[e]);
+    for (int k = 1; k < 8; ++k) sum += red[k][cl];
+    out[(int64_t)b * C + c] = sum;
   }
 }
 
@@ -419,26 +442,32 @@ int vd_upsample_nearest_hw_bwd(const void* dy, void* dx, int B, int T, int H, in
   });
 }
 
+size_t vd_channel_sums_workspace_size(int B, int C) {
+  if (B <= 0 || C <= 0) return 0;
+  return (size_t)B * kSumBlocks * C * sizeof(float);
+}
+
 int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dtype, float* out,
-                    void* stream) {
-  VD_REQUIRE(x && out, "null argument");
+                    void* workspace, void* stream) {
+  VD_REQUIRE(x && out && workspace, "null argument");
   VD_REQUIRE(B > 0 && S > 0 && C > 0 && C % 8 == 0 && C <= 2048, "bad shape B=%d C=%d", B, C);
   const int cs = cstride ? cstride : C;
   VD_REQUIRE(cs >= C && cs % 8 == 0, "bad channel stride %d", cs);
   hipStream_t st = VD_STREAM(stream);
-  if (hipMemsetAsync(out, 0, (size_t)B * C * sizeof(float), st) != hipSuccess)
-    return vd::fail(VD_ELAUNCH, "memset");
-  // ~4 blocks per CU over the whole batch
-  int64_t blocks = vd_cdiv(1024, B);
+  // about kSumBlocks blocks per sample, at least 4 row iterations each
   const int64_t rpi = 256 / (C / 8);
+  int64_t blocks = kSumBlocks;
   int64_t maxb = vd_cdiv(S, rpi * 4);
   if (blocks > maxb) blocks = maxb;
   if (blocks < 1) blocks = 1;
   const int64_t rows = vd_cdiv(S, blocks);
   blocks = vd_cdiv(S, rows);
+  float* part = reinterpret_cast<float*>(workspace);
   return VD_DISPATCH_DTYPE(dtype, Tp, {
     channel_sums_kernel<Tp><<<dim3((unsigned)blocks, (unsigned)B), 256, 0, st>>>(
-        (const Tp*)x, S, C, cs, rows, out);
+        (const Tp*)x, S, C, cs, rows, part);
+    channel_sums_finish_kernel<<<dim3((unsigned)vd_cdiv(C, 32), (unsigned)B), 256, 0, st>>>(
+        part, (int)blocks, C, out);
   });
 }
 

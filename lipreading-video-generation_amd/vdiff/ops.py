@@ -379,7 +379,9 @@ def channel_sums(x: torch.Tensor) -> torch.Tensor:
         x = _pad_channels(x, (Cc + 7) // 8 * 8)
     cp = x.shape[1]
     out = torch.empty(B, cp, dtype=torch.float32, device=x.device)
-    _lib.call("vd_channel_sums", _p(x), B, S, cp, 0, _dtype(x), _p(out), _stream(x))
+    ws = torch.empty(_lib.lib().vd_channel_sums_workspace_size(B, cp), dtype=torch.uint8,
+                     device=x.device)
+    _lib.call("vd_channel_sums", _p(x), B, S, cp, 0, _dtype(x), _p(out), _p(ws), _stream(x))
     return out[:, :Cc]
 
 
