@@ -1242,7 +1242,8 @@ int check_attn(const vd_attn_desc* d) {
 // Work shape per kernel: NB x 32 rows per wave, NW waves per workgroup.
 //   kNB2 : NB 2, NW 4 -- each LDS fragment feeds two MFMAs (bf16, D <= 128)
 //   kW8  : NB 1, NW 8 -- two waves per SIMD from one workgroup, each LDS tile shared by
-//          8 waves (bf16, D = 64; above that 2 waves/SIMD cannot hold the registers)
+//          8 waves (bf16, D <= 128; at D = 128 the 256-register budget holds dQ, while the
+//          forward spills and dK/dV needs a 64-column output slice per workgroup)
 //   kBase: NB 1, NW 4
 // VDIFF_ATTN_CFG=base|nb2|w8|p8|p4 overrides the choice for A/B measurements.
 //   kP8 / kP4: the software-pipelined kernels (tile_pipe) with 8 / 4 waves (bf16, D <= 128;
@@ -1267,12 +1268,12 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   AttnCfg c = kBase;
   // defaults = the fastest measured (tools/attn_bench.py, MI355X):
   //   D = 64 : fwd W8 17.2 ms, dQ P8 21.6 ms, dK/dV P8 29.1 ms (N = 262144)
-  //   D = 128: fwd NB2 2.0 ms, dQ P4 3.5 ms, dK/dV base 4.6 ms (N = 65536)
+  //   D = 128: fwd NB2 2.0 ms, dQ W8 2.8 ms (P4 3.7), dK/dV base 4.7 ms (N = 65536)
   if (env >= 0) c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kW8 : kP8;
-  else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kP4 : kBase);
+  else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kW8 : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
-  if (c == kW8 && D != 64) c = kBase;
+  if (c == kW8 && D > 128) c = kBase;
   if (c == kP8 && D != 64) c = kP4;
   if (c == kP4 && D > 128) c = kBase;
   return c;
@@ -1317,7 +1318,7 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
     const AttnCfg c = pick_cfg(D, true, 0);
     if constexpr (D != 256)
       if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, q, k, v, o, lse, st);
-    if constexpr (D == 64)
+    if constexpr (D <= 128)
       if (c == kW8) return fwd_launch<T, D, 1, 8>(d, q, k, v, o, lse, st);
     if constexpr (D == 64)
       if (c == kP8) return fwd_pipe_launch<T, D, 8>(d, q, k, v, o, lse, st);
@@ -1378,7 +1379,7 @@ int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void*
     const AttnCfg c = pick_cfg(D, true, 1);
     if constexpr (D != 256)
       if (c == kNB2) return dq_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
-    if constexpr (D == 64)
+    if constexpr (D <= 128)
       if (c == kW8) return dq_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kP8) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
@@ -1394,7 +1395,9 @@ int dkdv_launch(const vd_attn_desc* d, const void* q, const void* k, const void*
                 hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
-  constexpr int DO = D > 128 ? 128 : D;
+  // output-column slice per workgroup (grid.z = D / DO): register budget at D = 256, and at
+  // D = 128 with 8 waves (two per SIMD: 256 registers each)
+  constexpr int DO = D > 128 ? 128 : (D == 128 && NW == 8 ? 64 : D);
   const size_t lds = tile_loop_lds<T, D, true>();
   auto kern = attn_bwd_dkdv_kernel<T, D, DO, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1435,7 +1438,7 @@ int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const voi
     const AttnCfg c = pick_cfg(D, true, 2);
     if constexpr (D <= 64)
       if (c == kNB2) return dkdv_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
-    if constexpr (D == 64)
+    if constexpr (D <= 128)
       if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kP8) return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
