@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--cpu-size", type=int, default=32)
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--only", choices=["train", "ddim", "all"], default="all")
+    ap.add_argument("--c4-steps", type=int, default=1,
+                    help="timed DDIM steps at BASELINE config 4 (256x256x25); 0 skips the leg")
     return ap.parse_args()
 
 
@@ -293,6 +295,36 @@ def main():
                 "model_tflops_per_gpu": round(work.total / (el / kd) / 1e12, 1)}
         result["ddim"] = ddim
         log(f"ddim: {ddim['ms_per_step']} ms/step, {ddim['value']} steps/s")
+        if args.c4_steps > 0:
+            # BASELINE config 4: 256x256x25-frame UNet3D, 50-step DDIM (test.py path), one clip
+            # per GPU; the same weights (the UNet is size-agnostic), audio encoded once
+            T4, S4, k4 = 25, 256, args.c4_steps
+            work4 = unet_forward_work(model, (1, 195, T4, S4, S4))
+            clip4 = synthetic_clip(1, T4, S4, 500, device, seed=200 + rank)
+            with torch.no_grad():
+                feats4 = model.encode_audio(clip4.audio)
+                x4 = torch.randn_like(clip4.x0)
+                t = torch.full((1,), int(sampler.timesteps[0]), dtype=torch.int64, device=device)
+                x4, _ = sampler.step(x4, model(x4, clip4.cond, feats4, t), 0)  # warm-up step
+                barrier_sync(world)
+                t0 = time.perf_counter()
+                for i in range(1, 1 + k4):
+                    t = torch.full((1,), int(sampler.timesteps[i]), dtype=torch.int64,
+                                    device=device)
+                    x4, _ = sampler.step(x4, model(x4, clip4.cond, feats4, t), i)
+                barrier_sync(world)
+                el4 = max_over_ranks(time.perf_counter() - t0, world, device)
+            result["ddim_config4"] = {
+                "metric": "DDIM steps/sec, 256x256x25 UNet3D (BASELINE config 4, test.py path)",
+                "value": round(world * k4 / el4, 4), "unit": "steps/s",
+                "ms_per_step": round(el4 / k4 * 1e3, 1), "steps_timed": k4,
+                "attention_mode": args.mode, "fwd_tflop": round(work4.total / 1e12, 1),
+                "model_tflops_per_gpu": round(work4.total / (el4 / k4) / 1e12, 1),
+                "sampling_50_steps_s": round(50 * el4 / k4, 1)}
+            log(f"ddim config 4 (256x256x25): {result['ddim_config4']['ms_per_step']} ms/step, "
+                f"{result['ddim_config4']['model_tflops_per_gpu']} TFLOP/s")
+            del clip4, feats4, x4
+            torch.cuda.empty_cache()
         if "value" not in result:
             result.update(value=ddim["value"], unit="steps/s", ms_per_step=ddim["ms_per_step"])
 
