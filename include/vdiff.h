@@ -221,6 +221,15 @@ typedef struct vd_attn_desc {
 
 int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k,
                      const void* v, void* o, float* lse, void* stream);
+/* Same, with a workspace: where the query grid would leave CUs idle (bf16, e.g. head_dim 256
+ * at N = 16384) the keys are split over grid.z and the fp32 partials merged by a second
+ * kernel (flash-decoding style).  workspace_bytes < vd_attention_fwd_workspace_size(d)
+ * (which is 0 for shapes that do not split) falls back to vd_attention_fwd. */
+size_t vd_attention_fwd_workspace_size(const vd_attn_desc* d);
+int vd_attention_fwd_ws(const vd_attn_desc* d, const void* q, const void* k,
+                        const void* v, void* o, float* lse, void* workspace,
+                        size_t workspace_bytes, void* stream);
+/* Backward workspace: the row constants, plus the KV-split dQ partials for shapes that split. */
 size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d);
 /* Kernel shape used for bf16 (no effect on results beyond fp32 summation order):
  * -1 per-kernel default, 0 base (4 waves x 32 rows), 1 two 32-row blocks per wave,

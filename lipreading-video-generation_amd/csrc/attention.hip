@@ -663,15 +663,29 @@ size_t tile_loop_lds() {
 //    recomputed with its true max (rare path), which resets m and rescales O and l.
 constexpr float kLagSum = 65536.f;  // 2^16: p <= 2^16, l <= 2^16 * N -- far from overflow
 
+// KV split (flash-decoding style, for shapes whose query grid leaves CUs idle): workgroup
+// z of grid.z takes the key tiles [z * tps, (z + 1) * tps) and writes its unnormalised O^T
+// (fp32) and (m, l) to `part`; attn_fwd_combine_kernel merges the splits.  part == nullptr:
+// one split, normalised output as before.
+struct FwdSplit {
+  float* part;  // [splits][nseq][n][D] O (or dQ), then [splits][nseq][n][2] (m, l)
+  int tps;      // key tiles per split
+};
+
 template <typename T, int D, int NB, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
-    float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
+    float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale,
+    FwdSplit split) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
+  // this workgroup's keys: [kofs, kofs + nk)
+  const int kofs = blockIdx.z * split.tps * kTile;
+  const int nk = split.part ? min(n - kofs, split.tps * kTile) : n;
+  const int64_t kbase = base + (int64_t)kofs * ts;
 
   RowFrag<T, D> qf[NB];
 #pragma unroll
@@ -694,16 +708,16 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
     for (int r = 0; r < 16; ++r) negm[j][r] = INFINITY;
   }
 
-  tile_loop<T, D, false, NW>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
+  tile_loop<T, D, false, NW>(smem, k + kbase, v + kbase, ts, ts, nullptr, nullptr, nk, tid,
                          [&](int t, const T* Kt, const T* Vt, const float*) {
     const int key0 = t * kTile;
-    const bool tail = key0 + kTile > n;  // only the last tile masks keys (wave-uniform)
+    const bool tail = key0 + kTile > nk;  // only the last tile masks keys (wave-uniform)
     auto mask = [&](f32x16 (&s)[2][NB]) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (key0 + 32 * h + acc_row(r, hh) >= n)
+          if (key0 + 32 * h + acc_row(r, hh) >= nk)
 #pragma unroll
             for (int j = 0; j < NB; ++j) s[h][j][r] = -INFINITY;
     };
@@ -826,8 +840,55 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
     f32x16 out[D / 32];
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) out[i] = oacc[i][j];
-    store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, out, 1.f / lt, lane);
-    if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m[j] + log2f(lt)) / kLog2e;
+    if (split.part) {
+      const int64_t row0 = ((int64_t)blockIdx.z * gridDim.y + seq) * n;
+      store_transposed<float, D / 32>(split.part + row0 * D, D, myq, n, 0, out, 1.f, lane);
+      float* ml = split.part + (int64_t)gridDim.z * gridDim.y * n * D;
+      if (hh == 0 && myq < n) {
+        ml[(row0 + myq) * 2] = m[j];
+        ml[(row0 + myq) * 2 + 1] = lt;
+      }
+    } else {
+      store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, out, 1.f / lt, lane);
+      if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m[j] + log2f(lt)) / kLog2e;
+    }
+  }
+}
+
+// Merge the KV splits of attn_fwd_kernel: per query row, M = max m_z,
+// O = sum_z 2^(m_z - M) O_z / sum_z 2^(m_z - M) l_z, lse = (M + log2 L) / log2(e).
+// One thread per (row, 8 output columns).
+template <typename T, int D>
+__global__ void attn_fwd_combine_kernel(const float* __restrict__ part, int splits, int nseq,
+                                        int n, T* __restrict__ o, SeqAddr oa, int64_t ots,
+                                        float* __restrict__ lse) {
+  constexpr int CPR = D / 8;
+  const int64_t rows = (int64_t)nseq * n;
+  const float* ml = part + (int64_t)splits * rows * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * CPR;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / CPR;
+    const int c8 = (int)(i % CPR) * 8;
+    float mz[4], M = -INFINITY;
+    for (int z = 0; z < splits; ++z) {
+      mz[z] = ml[((int64_t)z * rows + row) * 2];
+      M = fmaxf(M, mz[z]);
+    }
+    float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int z = 0; z < splits; ++z) {
+      const float w = fast_exp2(mz[z] - M);
+      L += w * ml[((int64_t)z * rows + row) * 2 + 1];
+      float v8[8];
+      load8(part + ((int64_t)z * rows + row) * D + c8, v8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += w * v8[e];
+    }
+    const float inv = 1.f / L;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    const int seq = (int)(row / n), tok = (int)(row % n);
+    store8(o + oa(seq) + (int64_t)tok * ots + c8, acc);
+    if (c8 == 0) lse[row] = (M + log2f(L)) / kLog2e;
   }
 }
 
@@ -863,16 +924,22 @@ __global__ void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__
 // Q pre-scaled as in the forward; S' accumulator starts at -lse*log2(e) and dP^T at
 // -delta (per-lane splats, the query is on the lane), so P^T = exp2(acc) and
 // dS^T = P^T * acc_dP leave one exp and one multiply per score.
+// KV split as the forward: z takes key tiles [z * tps, (z + 1) * tps) and writes its
+// (scaled) fp32 dQ partial to part[z][nseq][n][D]; attn_dq_sum_kernel adds the splits.
 template <typename T, int D, int NB, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
     const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
-    T* __restrict__ dq, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
+    T* __restrict__ dq, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale,
+    FwdSplit split) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
+  const int kofs = blockIdx.z * split.tps * kTile;
+  const int nk = split.part ? min(n - kofs, split.tps * kTile) : n;
+  const int64_t kbase = base + (int64_t)kofs * ts;
 
   RowFrag<T, D> qf[NB], of[NB];
   f32x16 il[NB], id[NB];
@@ -896,7 +963,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_kernel(
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
 
-  tile_loop<T, D, false, NW>(smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid,
+  tile_loop<T, D, false, NW>(smem, k + kbase, v + kbase, ts, ts, nullptr, nullptr, nk, tid,
                          [&](int, const T* Kt, const T* Vt, const float*) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -926,7 +993,35 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_kernel(
     f32x16 out[D / 32];
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) out[i] = acc[i][j];
-    store_transposed<T, D / 32>(dq + base, ts, q0 + 32 * j + (lane & 31), n, 0, out, scale, lane);
+    if (split.part)
+      store_transposed<float, D / 32>(
+          split.part + ((int64_t)blockIdx.z * gridDim.y + seq) * n * D, D,
+          q0 + 32 * j + (lane & 31), n, 0, out, scale, lane);
+    else
+      store_transposed<T, D / 32>(dq + base, ts, q0 + 32 * j + (lane & 31), n, 0, out, scale,
+                                  lane);
+  }
+}
+
+// dq = sum over the KV splits of the fp32 partials (one thread per 8 columns)
+template <typename T, int D>
+__global__ void attn_dq_sum_kernel(const float* __restrict__ part, int splits, int nseq, int n,
+                                   T* __restrict__ dq, SeqAddr qa, int64_t ts) {
+  constexpr int CPR = D / 8;
+  const int64_t rows = (int64_t)nseq * n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * CPR;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / CPR;
+    const int c8 = (int)(i % CPR) * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int z = 0; z < splits; ++z) {
+      float v8[8];
+      load8(part + ((int64_t)z * rows + row) * D + c8, v8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v8[e];
+    }
+    const int seq = (int)(row / n), tok = (int)(row % n);
+    store8(dq + qa(seq) + (int64_t)tok * ts + c8, acc);
   }
 }
 
@@ -1273,26 +1368,63 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   else if (D == 64) c = kind == 0 ? kW8 : kP8;
   else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kW8 : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
-  if (c == kW8 && D > 128) c = kBase;
+  if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
   if (c == kP8 && D != 64) c = kP4;
   if (c == kP4 && D > 128) c = kBase;
   return c;
 }
 
+// KV splits for a query grid of `wgs` workgroups: enough to give every CU one (>= 256),
+// at most 4, at least 4 key tiles each; 1 = no split.  bf16 only.
+int kv_splits(const vd_attn_desc* d, int64_t wgs) {
+  if (d->dtype != VD_BF16 || wgs >= 256) return 1;
+  int s = (int)((256 + wgs - 1) / wgs);
+  if (s > 4) s = 4;
+  const int64_t tiles = vd_cdiv(d->seq_len, kTile);
+  while (s > 1 && tiles / s < 4) --s;
+  return s;
+}
+int split_tps(const vd_attn_desc* d, int s) {
+  return (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), s);
+}
+
 template <typename T, int D, int NB, int NW>
 int fwd_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
-               float* lse, hipStream_t st) {
+               float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
   const size_t lds = tile_loop_lds<T, D, false>();
   auto kern = attn_fwd_kernel<T, D, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq);
+  const int64_t qwg = vd_cdiv(d->seq_len, 32 * NB * NW);
+  int s = kv_splits(d, qwg * d->nseq);
+  const size_t need = (size_t)s * d->nseq * d->seq_len * (D + 2) * sizeof(float);
+  if (s > 1 && (!ws || ws_bytes < need)) s = 1;
+  FwdSplit split{s > 1 ? (float*)ws : nullptr, split_tps(d, s)};
+  if (s > 1) s = (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), split.tps);
+  dim3 grid((unsigned)qwg, (unsigned)d->nseq, (unsigned)s);
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
                                    d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
-                                   d->token_stride,
-                                   SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
-                                   d->o_token_stride, d->scale);
+                                   d->token_stride, oa, d->o_token_stride, d->scale, split);
+  if (s > 1) {
+    const int rc = vd::check_launch("attn_fwd");
+    if (rc) return rc;
+    const int64_t work = (int64_t)d->nseq * d->seq_len * (D / 8);
+    int g = (int)vd_cdiv(work, 256);
+    if (g > 4096) g = 4096;
+    attn_fwd_combine_kernel<T, D><<<g, 256, 0, st>>>(split.part, s, d->nseq, d->seq_len, (T*)o,
+                                                     oa, d->o_token_stride, lse);
+  }
   return vd::check_launch("attn_fwd");
+}
+
+// bytes of the KV-split forward workspace of this shape (0: no split is used)
+template <int D>
+size_t fwd_ws_bytes(const vd_attn_desc* d) {
+  if (d->dtype != VD_BF16) return 0;
+  if (pick_cfg(D, true, 0) != kBase) return 0;  // only the 4-wave, 32-row shape splits
+  const int s = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq);
+  return s > 1 ? (size_t)s * d->nseq * d->seq_len * (D + 2) * sizeof(float) : 0;
 }
 
 template <typename T, int D, int NW>
@@ -1313,35 +1445,48 @@ int fwd_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const v
 
 template <typename T, int D>
 int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
-             float* lse, hipStream_t st) {
+             float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
   if constexpr (kDMA<T>) {
     const AttnCfg c = pick_cfg(D, true, 0);
     if constexpr (D != 256)
-      if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, q, k, v, o, lse, st);
-    if constexpr (D <= 128)
-      if (c == kW8) return fwd_launch<T, D, 1, 8>(d, q, k, v, o, lse, st);
+      if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, q, k, v, o, lse, nullptr, 0, st);
+    if constexpr (D == 64 || D == 128)
+      if (c == kW8) return fwd_launch<T, D, 1, 8>(d, q, k, v, o, lse, nullptr, 0, st);
     if constexpr (D == 64)
       if (c == kP8) return fwd_pipe_launch<T, D, 8>(d, q, k, v, o, lse, st);
     if constexpr (D <= 128)
       if (c == kP4) return fwd_pipe_launch<T, D, 4>(d, q, k, v, o, lse, st);
   }
-  return fwd_launch<T, D, 1, 4>(d, q, k, v, o, lse, st);
+  return fwd_launch<T, D, 1, 4>(d, q, k, v, o, lse, ws, ws_bytes, st);
 }
 
 template <typename T, int D, int NB, int NW>
 int dq_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
               const void* dout, const float* nlse2, const float* ndelta, void* dq,
-              hipStream_t st) {
+              hipStream_t st, float* part = nullptr) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const size_t lds = tile_loop_lds<T, D, false>();
   auto kern = attn_bwd_dq_kernel<T, D, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq);
+  const int64_t qwg = vd_cdiv(d->seq_len, 32 * NB * NW);
+  int s = part ? kv_splits(d, qwg * d->nseq) : 1;
+  FwdSplit split{s > 1 ? part : nullptr, split_tps(d, s)};
+  if (s > 1) s = (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), split.tps);
+  dim3 grid((unsigned)qwg, (unsigned)d->nseq, (unsigned)s);
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
                                    ndelta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
-                                   d->o_token_stride, d->scale);
+                                   d->o_token_stride, d->scale, split);
+  if (s > 1) {
+    const int rc = vd::check_launch("attn_bwd_dq");
+    if (rc) return rc;
+    const int64_t work = (int64_t)d->nseq * d->seq_len * (D / 8);
+    int g = (int)vd_cdiv(work, 256);
+    if (g > 4096) g = 4096;
+    attn_dq_sum_kernel<T, D><<<g, 256, 0, st>>>(split.part, s, d->nseq, d->seq_len, (T*)dq, qa,
+                                               d->token_stride);
+  }
   return vd::check_launch("attn_bwd_dq");
 }
 
@@ -1379,14 +1524,17 @@ int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void*
     const AttnCfg c = pick_cfg(D, true, 1);
     if constexpr (D != 256)
       if (c == kNB2) return dq_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
-    if constexpr (D <= 128)
+    if constexpr (D == 64 || D == 128)
       if (c == kW8) return dq_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kP8) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D <= 128)
       if (c == kP4) return dq_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
   }
-  return dq_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+  // the 4-wave, 32-row shape splits the keys when its grid leaves CUs idle (bf16, D = 256):
+  // fp32 partials after the row constants in the workspace (vd_attention_bwd_workspace_size)
+  return dq_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st,
+                               kDMA<T> ? nlse2 + rows + 64 : nullptr);
 }
 
 template <typename T, int D, int NB, int NW>
@@ -1438,7 +1586,7 @@ int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const voi
     const AttnCfg c = pick_cfg(D, true, 2);
     if constexpr (D <= 64)
       if (c == kNB2) return dkdv_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
-    if constexpr (D <= 128)
+    if constexpr (D == 64 || D == 128)
       if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kP8) return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
@@ -1471,20 +1619,37 @@ int vd_debug_attn_stamps(void* dst, size_t bytes) {
 }
 #endif
 
-int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
-                     float* lse, void* stream) {
+int vd_attention_fwd_ws(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                        void* o, float* lse, void* workspace, size_t workspace_bytes,
+                        void* stream) {
   int rc = check_attn(d);
   if (rc) return rc;
   VD_REQUIRE(q && k && v && o && lse, "null tensor");
   hipStream_t st = VD_STREAM(stream);
   if (d->dtype == VD_BF16) {
     using T = bf16_t;
-    VD_DISPATCH_HEAD(d->head_dim, fwd_impl, d, q, k, v, o, lse, st);
+    VD_DISPATCH_HEAD(d->head_dim, fwd_impl, d, q, k, v, o, lse, workspace, workspace_bytes, st);
   } else if (d->dtype == VD_F32) {
     using T = float;
-    VD_DISPATCH_HEAD(d->head_dim, fwd_impl, d, q, k, v, o, lse, st);
+    VD_DISPATCH_HEAD(d->head_dim, fwd_impl, d, q, k, v, o, lse, workspace, workspace_bytes, st);
   }
   return vd::fail(VD_EUNSUPPORTED, "dtype %d", d->dtype);
+}
+
+int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
+                     float* lse, void* stream) {
+  return vd_attention_fwd_ws(d, q, k, v, o, lse, nullptr, 0, stream);
+}
+
+size_t vd_attention_fwd_workspace_size(const vd_attn_desc* d) {
+  if (!d || d->nseq <= 0 || d->seq_len <= 0) return 0;
+  switch (d->head_dim) {
+    case 32: return fwd_ws_bytes<32>(d);
+    case 64: return fwd_ws_bytes<64>(d);
+    case 128: return fwd_ws_bytes<128>(d);
+    case 256: return fwd_ws_bytes<256>(d);
+    default: return 0;
+  }
 }
 
 int vd_attention_set_config(int cfg) {
@@ -1497,7 +1662,14 @@ int vd_attention_set_config(int cfg) {
 
 size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d) {
   if (!d || d->nseq <= 0 || d->seq_len <= 0) return 0;
-  return 2 * (size_t)d->nseq * d->seq_len * sizeof(float) + 256;  // ndelta, nlse2
+  const size_t rows = (size_t)d->nseq * d->seq_len;
+  size_t bytes = 2 * rows * sizeof(float) + 256;  // ndelta, nlse2
+  // KV-split dQ partials (bf16, the 4-wave dQ shape when its grid leaves CUs idle)
+  if (d->dtype == VD_BF16 && pick_cfg(d->head_dim, true, 1) == kBase) {
+    const int s = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq);
+    if (s > 1) bytes += 64 * sizeof(float) + (size_t)s * rows * d->head_dim * sizeof(float);
+  }
+  return bytes;
 }
 
 int vd_attention_bwd_dq(const vd_attn_desc* d, const void* q, const void* k, const void* v,

@@ -68,6 +68,8 @@ _SIGS = {
     "vd_conv3d_bwd_data": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp]),
     "vd_conv3d_bwd_weight": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp]),
     "vd_attention_fwd": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp]),
+    "vd_attention_fwd_workspace_size": (_sz, [C.POINTER(AttnDesc)]),
+    "vd_attention_fwd_ws": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "vd_attention_bwd_workspace_size": (_sz, [C.POINTER(AttnDesc)]),
     "vd_attention_set_config": (C.c_int, [C.c_int]),
     "vd_attention_bwd": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

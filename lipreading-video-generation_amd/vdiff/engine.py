@@ -69,7 +69,10 @@ class Trainer:
         self.model = model
         self.scheduler = scheduler
         params = [p for p in model.parameters() if p.requires_grad]
-        self.bucketer = GradBucketer(params, bucket_mb)
+        # one process: no all-reduce, so no bucket views -- autograd hands each gradient over
+        # without the accumulate-into-view add, and zero_grad drops them (no fills)
+        distributed = torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1
+        self.bucketer = GradBucketer(params, bucket_mb) if distributed else None
         kw = {"fused": True} if fused_adam and params and params[0].is_cuda else {}
         self.opt = torch.optim.Adam(params, lr=lr, **kw)
 
@@ -79,9 +82,13 @@ class Trainer:
         pred = self.model(xt, clip.cond, clip.audio, clip.t)
         loss = F.mse_loss(pred, clip.eps)
         loss.backward()
-        self.bucketer.finish()
+        if self.bucketer is not None:
+            self.bucketer.finish()
         self.opt.step()
-        self.bucketer.zero_grad()
+        if self.bucketer is not None:
+            self.bucketer.zero_grad()
+        else:
+            self.opt.zero_grad(set_to_none=True)
         return loss.detach()
 
 

@@ -596,9 +596,11 @@ class AttentionFn(torch.autograd.Function):
         for d, qo, ko, vo, oo in launches:
             lse = torch.empty(d.nseq * d.seq_len, dtype=torch.float32, device=qkv.device)
             base = qkv.data_ptr()
+            nws = _lib.lib().vd_attention_fwd_workspace_size(d)  # KV-split partials, or 0
+            ws = torch.empty(nws, dtype=torch.uint8, device=qkv.device) if nws else None
             ev = _timer.begin() if _timer is not None else None
-            _lib.call("vd_attention_fwd", d, base + qo * es, base + ko * es, base + vo * es,
-                      out.data_ptr() + oo * es, _p(lse), _stream(qkv))
+            _lib.call("vd_attention_fwd_ws", d, base + qo * es, base + ko * es, base + vo * es,
+                      out.data_ptr() + oo * es, _p(lse), _p(ws), nws, _stream(qkv))
             if ev is not None:
                 _timer.end(ev, "attn_fwd", d)
             lses.append(lse)

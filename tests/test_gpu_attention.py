@@ -113,3 +113,12 @@ def test_golden_regroupings():
                       ("temporal", "st_temporal")):
         out = ops.attention(qkv, heads=1, mode=mode, spatial=(T, 6, 6))
         assert rel_l2(out, g[key]) < 2e-5, mode
+
+
+@pytest.mark.parametrize("C,T,HW", [(256, 4, 256), (64, 1, 1000)])
+def test_kv_split(C, T, HW):
+    """KV-split forward / dQ (flash-decoding partials + merge): the 4-wave shape splits the keys
+    when its query grid is too small for the chip (bf16, head_dim 256 by default)."""
+    from vdiff import ops
+    with ops.attention_config("base"):
+        _check(1, C, 1, T, HW, "joint", True, torch.bfloat16, 80 + C)
