@@ -422,6 +422,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgtGeom g, const T
 // during this step's MFMAs.
 constexpr int kIgBK = 64;
 // VDIFF_CONV_LEGACY=1: the previous k-major kernel for bf16 too (A/B measurements)
+// VDIFF_CONV_DMA=0: the register-staged tap-outer kernel instead of the LDS-DMA ring
+const bool g_conv_dma = [] {
+  const char* e = getenv("VDIFF_CONV_DMA");
+  return !(e && e[0] == '0');
+}();
 const bool g_legacy_conv = [] {
   const char* e = getenv("VDIFF_CONV_LEGACY");
   return e && e[0] == '1';
@@ -820,6 +825,223 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_bf16_kernel(
   }
 }
 
+// ----------------------------------------------------------------- bf16 implicit GEMM, LDS-DMA ring
+// Same GEMM and tap-major K walk as igemm_bf16_kernel, but the A rows (gathered pixels) and
+// B rows (packed weights) go global -> LDS by buffer_load ... lds, in 1-KiB pieces of 8
+// rows x 128 B, into an NST-stage ring two K steps ahead.  Staging through registers cost
+// a ds_write_b128 per 16 B (13 LDS cycles each, MI355X_MICROARCH.md "LDS") -- more LDS time
+// than the MFMAs it fed; the DMA needs no VGPRs and no store instructions.  The ring is
+// ordered by a counted vmcnt and one barrier per step; steps past the end issue out-of-range
+// (zero-fill, no traffic) pieces so every wait counts the same.  Lane l of a piece writes row
+// l / 8, physical chunk l % 8; it fetches logical chunk (l % 8) ^ ((row >> 1) & 7), so the
+// LDS image is the XOR-swizzled one ig_off() reads.  A source pixel outside the image (the
+// tap bit is clear) gets an offset past the buffer end and reads zeros.
+template <int BM, int BN, int WAVES_M, bool TR, int NST>
+__global__ __launch_bounds__(kThreads, 2) void igemm_dma_kernel(
+    GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
+    bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
+    const bf16_t* __restrict__ residual) {
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int NI = WTM / 16, NJ = WTN / 16;
+  constexpr int IA = BM / 32, IB = BN / 32;  // pieces per wave per step (A, B)
+  constexpr int PIECES = IA + IB;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bf16_t* lds = reinterpret_cast<const bf16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int C = g.sC;
+  const int taps = g.kt * g.kh * g.kw, khw = g.kh * g.kw;
+  const int csteps = (C + kIgBK - 1) / kIgBK;
+  const int nk = taps * csteps;
+  const int lr = lane >> 3, pc = lane & 7;
+
+  // this lane's A rows (one per piece): source byte offset at tap 0 incl. its chunk, the
+  // tap-validity bits, and the chunk's first channel
+  int a_off[IA], a_c[IA];
+  uint32_t a_ok[IA];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int r = (wave * IA + i) * 8 + lr;
+    const int c = pc ^ ((r >> 1) & 7);
+    a_c[i] = c * 8;
+    int m = (int)m0 + r;
+    const bool in = m < (int)g.M;
+    if (!in) m = 0;
+    const int w = m % g.dW; m /= g.dW;
+    const int h = m % g.dH; m /= g.dH;
+    const int t = m % g.dT;
+    const int b = m / g.dT;
+    int bt, bh, bw;
+    if (!TR) {
+      bt = t * g.st - g.pt; bh = h * g.sh - g.ph; bw = w * g.sw - g.pw;
+    } else {
+      bt = t + g.pt; bh = h + g.ph; bw = w + g.pw;
+    }
+    uint32_t vt = 0, vh = 0, vw = 0;
+    for (int a = 0; a < g.kt; ++a) vt |= (uint32_t)((unsigned)(TR ? bt - a : bt + a) < (unsigned)g.sT) << a;
+    for (int a = 0; a < g.kh; ++a) vh |= (uint32_t)((unsigned)(TR ? bh - a : bh + a) < (unsigned)g.sH) << a;
+    for (int a = 0; a < g.kw; ++a) vw |= (uint32_t)((unsigned)(TR ? bw - a : bw + a) < (unsigned)g.sW) << a;
+    uint32_t ok = 0;
+    for (int a = 0; a < g.kt; ++a)
+      for (int c2 = 0; c2 < g.kh; ++c2)
+        if (((vt >> a) & (vh >> c2) & 1u) != 0) ok |= vw << (a * khw + c2 * g.kw);
+    a_ok[i] = in ? ok : 0u;
+    a_off[i] = (((b * g.sT + bt) * g.sH + bh) * g.sW + bw) * g.sCs * 2 + c * 16;
+  }
+  int b_off[IB], b_c[IB];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int r = (wave * IB + i) * 8 + lr;
+    const int c = pc ^ ((r >> 1) & 7);
+    b_c[i] = c * 8;
+    const int n = n0 + r;
+    b_off[i] = n < g.N ? n * g.K * 2 + c * 16 : (int)0x80000000;
+  }
+  const rsrc_t rs_a = make_rsrc(src, (uint32_t)((int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2));
+  const rsrc_t rs_b = make_rsrc(wt, (uint32_t)((int64_t)g.N * g.K * 2));
+
+  auto issue = [&](int s) {  // K step s into ring stage s % NST
+    char* st = smem + (s % NST) * STAGE;
+    const bool live = s < nk;
+    const int tap = live ? s / csteps : 0;
+    const int c0 = live ? (s - tap * csteps) * kIgBK : 0;
+    const int ta = tap / khw, rem = tap - ta * khw;
+    const int tb = rem / g.kw, tc = rem - tb * g.kw;
+    const int toff = ((ta * g.sH + tb) * g.sW + tc) * g.sCs * 2;
+    const int astep = (TR ? -toff : toff) + c0 * 2;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const bool ok = live && c0 + a_c[i] < C && ((a_ok[i] >> tap) & 1u);
+      dma_lds<16>(rs_a, lds_addr(st + (wave * IA + i) * 1024),
+                  ok ? (uint32_t)(a_off[i] + astep) : 0x80000000u);
+    }
+    const int bstep = (tap * C + c0) * 2;
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const bool ok = live && c0 + b_c[i] < C;
+      dma_lds<16>(rs_b, lds_addr(st + A_BYTES + (wave * IB + i) * 1024),
+                  ok ? (uint32_t)(b_off[i] + bstep) : 0x80000000u);
+    }
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  vm_drain();
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    vm_wait_barrier<(NST - 2) * PIECES>();  // step kt landed everywhere; step kt-1 consumed
+    issue(kt + NST - 1);
+    const bf16_t* As = lds + (kt % NST) * (STAGE / 2);
+    const bf16_t* Bs = As + A_BYTES / 2;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[NI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + ig_off(wm * WTM + 16 * i + fr, 4 * s + fq));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ig_off(wn * WTN + 16 * j + fr, 4 * s + fq));
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  vm_drain();  // the zero-fill pieces past the end land before the epilogue reuses LDS
+  __syncthreads();
+
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int LDC = BN + 4;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WTM + 16 * i + fq * 4 + r) * LDC + wn * WTN + 16 * j + fr] = acc[i][j][r];
+  __syncthreads();
+  const int64_t pix_per_b = (int64_t)g.dT * g.dH * g.dW;
+  const bool vec = (g.N % 8 == 0) && (g.dNs % 8 == 0);
+  for (int v = tid; v < BM * BN / 8; v += kThreads) {
+    const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+    const int64_t m = m0 + r;
+    const int n = n0 + c;
+    if (m >= g.M || n >= g.N) continue;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
+    const int bidx = (int)(m / pix_per_b);
+    const int lim = g.N - n < 8 ? g.N - n : 8;
+    if (bias)
+      for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
+    if (chan_add)
+      for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)bidx * g.N + n + e];
+    bf16_t* out = dst + m * g.dNs + n;
+    if (vec) {
+      if (residual) {
+        float rv[8];
+        load8(residual + m * g.dNs + n, rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rv[e];
+      }
+      store8(out, o);
+    } else {
+      for (int e = 0; e < lim; ++e) {
+        float val = o[e];
+        if (residual) val += bf2f(residual[m * g.dNs + n + e]);
+        out[e] = f2bf(val);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, bool TR, int NST>
+void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
+                const float* ca, const void* res, hipStream_t st) {
+  const size_t lds_ab = (size_t)NST * (BM + BN) * 128;
+  const size_t lds_c = (size_t)BM * (BN + 4) * 4;
+  const size_t lds = lds_ab > lds_c ? lds_ab : lds_c;
+  auto kern = igemm_dma_kernel<BM, BN, WM, TR, NST>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(g.M, BM), (unsigned)vd_cdiv(g.N, BN));
+  kern<<<grid, kThreads, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias,
+                                    ca, (const bf16_t*)res);
+}
+
+#ifndef VD_CDMA_SMALL_NST
+#define VD_CDMA_SMALL_NST 3
+#endif
+template <bool TR>
+int launch_igemm_dma(const GemmGeom& g, const void* src, const void* wt, void* dst,
+                     const float* bias, const float* ca, const void* res, hipStream_t st) {
+  // two workgroups per CU (double-buffered ring): measured faster than one workgroup with a
+  // three-stage ring on every UNet shape (tools/conv_ab4.sh).  N that is a multiple of 64 but
+  // not of 128 (the qkv conv, N = 192) takes 64-wide tiles: no half-empty column tile.
+  if (g.N <= 64 || (g.N % 128 != 0 && g.N % 64 == 0)) {
+    launch_igd<256, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+  } else if (vd_cdiv(g.M, 128) * vd_cdiv(g.N, 128) < 256) {
+    launch_igd<64, 128, 2, TR, VD_CDMA_SMALL_NST>(g, src, wt, dst, bias, ca, res, st);
+  } else {
+    launch_igd<128, 128, 2, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+  }
+  return VD_OK;
+}
+
 int check_desc(const vd_conv_desc* d) {
   VD_REQUIRE(d, "null descriptor");
   VD_REQUIRE(d->B > 0 && d->Ti > 0 && d->Hi > 0 && d->Wi > 0 && d->Ci > 0 && d->To > 0 &&
@@ -843,6 +1065,13 @@ template <typename T, bool TR>
 int launch_gemm(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
                 const float* ca, const void* res, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
+    const bool unit = g.st == 1 && g.sh == 1 && g.sw == 1;
+    // LDS-DMA ring: 32-bit buffer offsets, taps <= 32 (validity bits), unit-stride gather
+    // when transposed
+    if (!g_legacy_conv && g_conv_dma && g.kt * g.kh * g.kw <= 32 && (!TR || unit) &&
+        (int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2 < ((int64_t)1 << 31) &&
+        (int64_t)g.N * g.K * 2 < ((int64_t)1 << 31))
+      return launch_igemm_dma<TR>(g, src, wt, dst, bias, ca, res, st);
     if (!g_legacy_conv) return launch_igemm<TR>(g, src, wt, dst, bias, ca, res, st);
   }
   const int64_t mt = vd_cdiv(g.M, 128);

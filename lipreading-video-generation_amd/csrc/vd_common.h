@@ -106,3 +106,40 @@ __device__ __forceinline__ float wave_sum(float v) {
   }()
 
 static inline int64_t vd_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- LDS-DMA (buffer_load ... lds)
+// shared by the attention ring and the conv GEMM
+typedef __attribute__((address_space(3))) void lds_void;
+// Buffer resource words: base, stride 0, num_records = bytes (the range check zero-fills
+// beyond it), raw dword format.
+typedef int __attribute__((ext_vector_type(4))) rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  return rsrc_t{(int)(uint32_t)a, (int)(uint32_t)((a >> 32) & 0xffff), (int)bytes, 0x00020000};
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(const lds_void*)p;
+}
+
+// The LDS-DMA is issued from inline asm on purpose: the compiler's waitcnt pass cannot tell
+// which LDS bytes a builtin buffer_load...lds writes, so it put an s_waitcnt vmcnt(0) in
+// front of the first LDS read after it -- draining the whole ring every tile.  The ring's
+// own counted vmcnt + s_barrier (vm_wait_barrier) is what orders these writes.
+template <int BYTES>
+__device__ __forceinline__ void dma_lds(rsrc_t rs, uint32_t lds, uint32_t voff) {
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+                 ::"s"(lds), "v"(voff), "s"(rs));
+  else
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+                 ::"s"(lds), "v"(voff), "s"(rs));
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+// compiler-visible (the waitcnt pass then knows every earlier global load has landed and
+// puts no waits of its own inside the ring loop); 0x0F70 = vmcnt(0), expcnt/lgkmcnt untouched
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
