@@ -265,7 +265,7 @@ def main():
             k: {"launches": c, "ms_per_step": round(t / args.steps, 2),
                 "tflops": round(f / (t / 1e3) / 1e12, 1) if t > 0 else None}
             for k, (c, t, f) in sorted(by_kind.items())}
-        for (kind, key), (cnt, tot, flop) in sorted(conv.items(), key=lambda kv: -kv[1][1])[:24]:
+        for (kind, key), (cnt, tot, flop) in sorted(conv.items(), key=lambda kv: -kv[1][1])[:60]:
             log(f"  conv {kind:16s} {key:40s} x{cnt // args.steps:<3d} {tot / args.steps:7.2f} ms/step "
                 f"{flop * cnt / (tot / 1e3) / 1e12:7.1f} TF/s")
         del trainer

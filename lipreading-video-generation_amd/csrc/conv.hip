@@ -825,6 +825,216 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_bf16_kernel(
   }
 }
 
+// ----------------------------------------------------------- bf16 weight gradient, kw-strip, DMA
+// wgrad_bf16_kernel's tiling (three kw taps share one dY tile and one X strip) with the
+// operands staged global -> LDS by buffer_load ... lds into an NST-stage ring, as
+// igemm_dma_kernel: the register-staged version spent more LDS cycles on ds_write_b128 than
+// on the transposed reads the MFMAs need.  LDS rows are 128 B (64 channels) unpadded; the
+// 16-B chunk c of row r sits at c ^ wg_swz(r), which keeps the ds_read_b64_tr_b16 pattern
+// (rows b..b+3 and b+8..b+11 in one 32-lane group, for any b) free of bank conflicts.
+// COT output channels per workgroup (64 or 128, split in COT / 64 planes of 64 rows).
+__device__ __forceinline__ int wg_swz(int r) {
+  const int u = r >> 1;
+  return ((u + 2 * (u >> 2)) & 3) << 1;
+}
+__device__ __forceinline__ int wg_off(int r, int c) {  // element offset of channel c, row r
+  return r * 64 + ((((c >> 3) ^ wg_swz(r)) << 3) | (c & 7));
+}
+
+template <int RW, int COT, int NST, bool ONE>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
+__global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
+    WgtGeom g, int wc, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+    float* __restrict__ dw) {
+  constexpr int PY = COT / 32, PX = RW / 32;  // pieces per wave per step
+  constexpr int PIECES = PY + PX;
+  constexpr int Y_BYTES = COT * 128, STAGE = (COT + RW) * 128;
+  constexpr int WTM = COT / 2, NI = WTM / 16;
+  constexpr int NT = ONE ? 1 : 3;  // taps per workgroup
+  static_assert(!ONE || RW == 64, "1x1: the X tile is the step's 64 pixels");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bf16_t* lds = reinterpret_cast<const bf16_t*>(smem);
+
+  const int co_tiles = (g.Co + COT - 1) / COT, ci_tiles = (g.Ci + 63) / 64;
+  int bid = blockIdx.x;
+  const int cot = bid % co_tiles; bid /= co_tiles;
+  const int cit = bid % ci_tiles; bid /= ci_tiles;
+  const int tab = bid;
+  const int ta = tab / g.kh, tb = tab % g.kh;
+  const int co0 = cot * COT, ci0 = cit * 64;
+  const int64_t mbeg = (int64_t)blockIdx.y * g.m_per_split;
+  int64_t mend = mbeg + g.m_per_split;
+  if (mend > g.M) mend = g.M;
+  if (mbeg >= mend) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane >> 3, pc = lane & 7;
+  const int R = 64 / wc, SW = wc + 2;
+  // dY pieces: plane (wave * PY + i) / 8, pixel row ((wave * PY + i) % 8) * 8 + lr
+  int y_p[PY], y_col[PY];
+#pragma unroll
+  for (int i = 0; i < PY; ++i) {
+    const int pi = wave * PY + i;
+    const int p = (pi & 7) * 8 + lr;
+    const int c = pc ^ wg_swz(p);
+    y_p[i] = p;
+    y_col[i] = co0 + (pi >> 3) * 64 + c * 8;
+  }
+  // X pieces: strip row sr -> step row rr and strip column j (pixel w0 + j - 1)
+  int x_rr[PX], x_j[PX], x_col[PX];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    const int sr = (wave * PX + i) * 8 + lr;
+    if (ONE) {
+      x_rr[i] = 0;
+      x_j[i] = sr;
+      x_col[i] = ci0 + (pc ^ wg_swz(sr)) * 8;
+      continue;
+    }
+    x_rr[i] = sr / SW;
+    x_j[i] = sr - x_rr[i] * SW;
+    if (x_rr[i] >= R) x_rr[i] = -1;
+    x_col[i] = ci0 + (pc ^ wg_swz(sr)) * 8;
+  }
+  const rsrc_t rs_y = make_rsrc(dy, (uint32_t)(g.M * g.yCs * 2));
+  const rsrc_t rs_x = make_rsrc(x, (uint32_t)((int64_t)g.B * g.Ti * g.Hi * g.Wi * g.xCs * 2));
+
+  // first pixel of the step being issued (incremental)
+  int cb, ct, chh, cw;
+  {
+    int64_t m = mbeg;
+    cw = (int)(m % g.Wo); m /= g.Wo;
+    chh = (int)(m % g.Ho); m /= g.Ho;
+    ct = (int)(m % g.To);
+    cb = (int)(m / g.To);
+  }
+  const int nsteps = (int)((mend - mbeg + 63) / 64);
+  auto issue = [&](int s) {
+    char* st = smem + (s % NST) * STAGE;
+    const bool live = s < nsteps;
+    const int64_t ms = mbeg + (int64_t)s * 64;
+#pragma unroll
+    for (int i = 0; i < PY; ++i) {
+      const bool ok = live && ms + y_p[i] < mend && y_col[i] < g.Co;
+      dma_lds<16>(rs_y, lds_addr(st + (wave * PY + i) * 1024),
+                  ok ? (uint32_t)(((ms + y_p[i]) * g.yCs + y_col[i]) * 2) : 0x80000000u);
+    }
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      uint32_t off = 0x80000000u;
+      if (ONE) {
+        if (live && ms + x_j[i] < mend && x_col[i] < g.Ci)
+          off = (uint32_t)(((ms + x_j[i]) * g.xCs + x_col[i]) * 2);
+      } else if (live && x_rr[i] >= 0 && x_col[i] < g.Ci) {
+        int b = cb, t = ct, h = chh + x_rr[i];
+        while (h >= g.Ho) {
+          h -= g.Ho;
+          if (++t == g.To) {
+            t = 0;
+            ++b;
+          }
+        }
+        const int ti = t - g.pt + ta, hi = h - g.ph + tb, wi = cw + x_j[i] - g.pw;
+        if (b < g.B && (unsigned)ti < (unsigned)g.Ti && (unsigned)hi < (unsigned)g.Hi &&
+            (unsigned)wi < (unsigned)g.Wi) {
+          const int64_t pix = (((int64_t)b * g.Ti + ti) * g.Hi + hi) * g.Wi + wi;
+          off = (uint32_t)((pix * g.xCs + x_col[i]) * 2);
+        }
+      }
+      dma_lds<16>(rs_x, lds_addr(st + Y_BYTES + (wave * PX + i) * 1024), off);
+    }
+    if (!ONE && live) {  // advance by 64 pixels
+      cw += 64;
+      while (cw >= g.Wo) {
+        cw -= g.Wo;
+        if (++chh == g.Ho) {
+          chh = 0;
+          if (++ct == g.To) {
+            ct = 0;
+            ++cb;
+          }
+        }
+      }
+    }
+  };
+
+  // wave tile: co [WTM wm, +WTM) x ci [32 wn, +32) x 3 taps
+  const int wm = wave & 1, wn = wave >> 1;
+  f32x4 acc[NT][NI][2];
+#pragma unroll
+  for (int tc = 0; tc < NT; ++tc)
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[tc][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  vm_drain();
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s);
+  const int fr = lane & 15, fq = lane >> 4, q4 = fr >> 2, p4 = fr & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    vm_wait_barrier<(NST - 2) * PIECES>();
+    issue(s + NST - 1);
+    const bf16_t* Ys = lds + (s % NST) * (STAGE / 2);
+    const bf16_t* Xs = Ys + Y_BYTES / 2;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p_lo = 32 * ks + 8 * fq + q4, p_hi = p_lo + 4;
+      bf16x8 af[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int c = wm * WTM + 16 * i + 4 * p4;
+        const bf16_t* plane = Ys + (c >> 6) * 4096;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_bf16x4*)(plane + wg_off(p_lo, c & 63)));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_bf16x4*)(plane + wg_off(p_hi, c & 63)));
+        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int s_lo = ONE ? p_lo : (p_lo / wc) * SW + p_lo % wc;
+      const int s_hi = ONE ? p_hi : (p_hi / wc) * SW + p_hi % wc;
+#pragma unroll
+      for (int tc = 0; tc < NT; ++tc) {
+        bf16x8 bfr[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = wn * 32 + 16 * j + 4 * p4;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(Xs + wg_off(s_lo + tc, c)));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(Xs + wg_off(s_hi + tc, c)));
+          bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[tc][i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[tc][i][j], 0, 0, 0);
+      }
+    }
+  }
+  vm_drain();
+  const int taps = g.kt * g.kh * g.kw;
+  const int64_t krow = (int64_t)taps * g.Ci;
+#pragma unroll
+  for (int tc = 0; tc < NT; ++tc) {
+    const int tap = ONE ? 0 : tab * g.kw + tc;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = ci0 + wn * 32 + 16 * j + fr;
+        if (ci >= g.Ci) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wm * WTM + 16 * i + fq * 4 + r;
+          if (co < g.Co) atomicAdd(dw + (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
+        }
+      }
+  }
+}
+
 // ----------------------------------------------------------------- bf16 implicit GEMM, LDS-DMA ring
 // Same GEMM and tap-major K walk as igemm_bf16_kernel, but the A rows (gathered pixels) and
 // B rows (packed weights) go global -> LDS by buffer_load ... lds, in 1-KiB pieces of 8
@@ -1165,6 +1375,46 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
                      (d->kt == 1 || d->kt == 3) && d->st == 1 && d->sh == 1 && d->sw == 1 &&
                      d->pt == d->kt / 2 && d->ph == 1 && d->pw == 1 &&
                      (d->Wo % 64 == 0 || (64 % d->Wo == 0 && 64 / d->Wo <= d->Ho));
+  const bool one = d->dtype == VD_BF16 && !g_legacy_conv && taps == 1 && d->st == 1 &&
+                   d->sh == 1 && d->sw == 1 && d->pt == 0 && d->ph == 0 && d->pw == 0;
+  const int64_t x_bytes = (int64_t)d->B * d->Ti * d->Hi * d->Wi * g.xCs * 2;
+  const bool dma = g_conv_dma && (strip || one) && g.xCs % 8 == 0 && g.yCs % 8 == 0 &&
+                   x_bytes < (1ll << 31) && g.M * g.yCs * 2 < (1ll << 31);
+  hipStream_t st = VD_STREAM(stream);
+  if (dma) {
+    // LDS-DMA kernels: kw-strip (three taps per workgroup) or 1x1 (a plain GEMM over pixels)
+    const int wc = one ? 64 : (d->Wo < 64 ? d->Wo : 64);
+    const int rows = one ? 64 : (64 / wc) * (wc + 2);
+    const int cot = 64;
+    const int64_t tiles =
+        (int64_t)vd_cdiv(d->Co, cot) * vd_cdiv(d->Ci, 64) * (one ? 1 : d->kt * d->kh);
+    // ~2048 workgroups, but at least 32 K steps each for the strip kernel (shorter pixel
+    // ranges lose more to the ring's fill and the atomic epilogue than they gain in
+    // occupancy: 64->64 at 128x128 0.13 -> 0.116 ms, tools/conv_ab.sh)
+    int64_t splits = vd_cdiv(2048, tiles);
+    int64_t maxs = vd_cdiv(g.M, one ? 1024 : 2048);
+    if (splits > maxs) splits = maxs;
+    if (splits < 1) splits = 1;
+    g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
+    splits = vd_cdiv(g.M, g.m_per_split);
+    dim3 grid((unsigned)tiles, (unsigned)splits);
+#define VD_WGD(RW, COT, NST, ONE)                                                          \
+  do {                                                                                     \
+    auto kern = wgrad_dma_kernel<RW, COT, NST, ONE>;                                       \
+    const int lds = NST * (COT + RW) * 128;                                                \
+    (void)hipFuncSetAttribute((const void*)kern,                                           \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
+    kern<<<grid, kThreads, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);     \
+  } while (0)
+    // 64 x 64 tiles, double-buffered (40 KiB at RW = 96: three workgroups per CU).
+    // Measured against COT = 128 and a three-stage ring: both slower (tools/conv_ab.sh).
+    if (one) VD_WGD(64, 64, 2, true);
+    else if (rows <= 96) VD_WGD(96, 64, 2, false);
+    else if (rows <= 128) VD_WGD(128, 64, 2, false);
+    else VD_WGD(192, 64, 2, false);
+#undef VD_WGD
+    return vd::check_launch("conv_wgrad_dma");
+  }
   if (strip) {
     const int wc = d->Wo < 64 ? d->Wo : 64;
     const int rows = (64 / wc) * (wc + 2);
@@ -1176,7 +1426,6 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
     splits = vd_cdiv(g.M, g.m_per_split);
     dim3 grid((unsigned)tiles, (unsigned)splits);
-    hipStream_t st = VD_STREAM(stream);
 #define VD_WG(RW)                                                                        \
   wgrad_bf16_kernel<RW><<<grid, kThreads, 2 * (64 + RW) * 72 * 2, st>>>(                \
       g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw)
