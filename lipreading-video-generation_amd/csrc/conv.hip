@@ -1233,19 +1233,17 @@ void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, c
                                     ca, (const bf16_t*)res);
 }
 
-#ifndef VD_CDMA_SMALL_NST
-#define VD_CDMA_SMALL_NST 3
-#endif
 template <bool TR>
 int launch_igemm_dma(const GemmGeom& g, const void* src, const void* wt, void* dst,
                      const float* bias, const float* ca, const void* res, hipStream_t st) {
-  // two workgroups per CU (double-buffered ring): measured faster than one workgroup with a
+  // two or more workgroups per CU (double-buffered ring): measured faster than one workgroup with a
   // three-stage ring on every UNet shape (tools/conv_ab4.sh).  N that is a multiple of 64 but
   // not of 128 (the qkv conv, N = 192) takes 64-wide tiles: no half-empty column tile.
   if (g.N <= 64 || (g.N % 128 != 0 && g.N % 64 == 0)) {
     launch_igd<256, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
-  } else if (vd_cdiv(g.M, 128) * vd_cdiv(g.N, 128) < 256) {
-    launch_igd<64, 128, 2, TR, VD_CDMA_SMALL_NST>(g, src, wt, dst, bias, ca, res, st);
+  } else if (vd_cdiv(g.M, 128) * vd_cdiv(g.N, 128) < 512) {
+    // fewer than two 128 x 128 tiles per CU: 64 x 128 (256->256 at 16x32x32: 1.00 -> 0.91 ms)
+    launch_igd<64, 128, 2, TR, 2>(g, src, wt, dst, bias, ca, res, st);
   } else {
     launch_igd<128, 128, 2, TR, 2>(g, src, wt, dst, bias, ca, res, st);
   }
