@@ -369,15 +369,15 @@ template <typename T> constexpr bool kDMA = sizeof(T) == 2;
 
 template <int D> constexpr int nstage() { return D <= 64 ? 4 : (D == 128 ? 3 : 2); }
 // DMA instructions (1 KiB each) per wave per tile
-template <int D, int NW> constexpr int dma_ipw() { return kTile * D * 2 / 1024 / NW; }
+template <int D, int NW, int TR = kTile> constexpr int dma_ipw() { return TR * D * 2 / 1024 / NW; }
 
-// this wave's share of one [64 x D] bf16 tile: logical 16-B chunk c of row r lands at the
+// this wave's share of one [TR x D] bf16 tile: logical 16-B chunk c of row r lands at the
 // swizzled position toff(r, 8c) (the DMA writes lane-linearly, so the SOURCE chunk is
 // permuted by the same involution)
-template <int D, int NW>
+template <int D, int NW, int TR = kTile>
 __device__ __forceinline__ void dma_tile(rsrc_t rs, char* lds, int tok0, int n,
                                          uint32_t ts_bytes, int wave, int lane) {
-  constexpr int CPL = D / 8, RPI = 64 / CPL, IPW = dma_ipw<D, NW>();
+  constexpr int CPL = D / 8, RPI = 64 / CPL, IPW = dma_ipw<D, NW, TR>();
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
     const int gi = wave * IPW + i;
@@ -507,8 +507,9 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
 template <typename T> struct BlockRef {
   const T* a;       // stream a rows of the block's tile (K for fwd / dQ, Q for dK/dV)
   const T* b;       // stream b rows (V, or dO)
-  const float* rc;  // row constants of the tile (dK/dV)
-  int row0;         // 0 or 32: the block's rows within its tile
+  const float* rc;  // row constants of the tile (dK/dV): rc0 rows ...
+  const float* rc1; // ... and rc1 rows
+  int row0;         // 0, 32 (, 64, 96): the block's rows within its tile
   int idx;          // block index: rows [32 idx, 32 idx + 32) of the sequence
 };
 
@@ -532,19 +533,29 @@ template <int SR, int SM, int GR, int GM, int VP> struct BlockSched {
 };
 using NoSched = BlockSched<0, 0, 0, 0, 0>;
 
-template <typename T, int D, bool RC, int NW, typename SCH = NoSched, typename SF, typename GF,
-          typename VF>
+// TR: rows per LDS tile (64, or 128 = four blocks per tile, half the barriers per row).
+// Row constants (RC) of a tile: rc0 [TR floats] | rc1 [TR floats] | a 256-B throw-away slot.
+template <int D, bool RC, int TR = kTile>
+constexpr int pipe_stage_bytes() { return 2 * TR * D * 2 + (RC ? 2 * TR * 4 + 256 : 0); }
+
+template <typename T, int D, bool RC, int NW, typename SCH = NoSched, int TR = kTile,
+          typename SF, typename GF, typename VF>
 __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, int64_t ts_a,
                                           int64_t ts_b, const float* rc0, const float* rc1,
                                           int n, int tid, bool late, SF&& S, GF&& G, VF&& V) {
   static_assert(kDMA<T> && D <= 128, "pipelined ring: bf16, D <= 128");
-  constexpr int TE = tile_elems<T, D>();
+  static_assert(TR == 64 || TR == 128, "64- or 128-row tiles");
+  constexpr int TE = TR * D;     // bf16 elements per tile
+  constexpr int BPT = TR / 32;   // 32-row blocks per tile
+  constexpr int LB = BPT == 2 ? 1 : 2;
   constexpr int NST = 4, PD = 2;
-  constexpr int STAGE_BYTES = 2 * TE * 2 + (RC ? 768 : 0);
-  constexpr int PER_TILE = 2 * dma_ipw<D, NW>() + (RC ? 1 : 0);
+  constexpr int STAGE_BYTES = pipe_stage_bytes<D, RC, TR>();
+  constexpr int NRC = 2 * TR / 64;  // 64-dword row-constant pieces per tile
+  static_assert(!RC || NW >= NRC, "one row-constant piece per wave");
+  constexpr int PER_TILE = 2 * dma_ipw<D, NW, TR>() + (RC ? 1 : 0);
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntiles = (n + kTile - 1) / kTile;
+  const int ntiles = (n + TR - 1) / TR;
   const auto ra = make_rsrc(a, seq_bytes(n, ts_a, D, 2));
   const auto rb = make_rsrc(b, seq_bytes(n, ts_b, D, 2));
   rsrc_t r0, r1;
@@ -555,18 +566,22 @@ __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, in
   const uint32_t tsa = (uint32_t)(ts_a * 2), tsb = (uint32_t)(ts_b * 2);
   auto issue = [&](int t) {
     char* st = smem + (t % NST) * STAGE_BYTES;
-    const int tok0 = t * kTile;
-    dma_tile<D, NW>(ra, st, tok0, n, tsa, wave, lane);
-    dma_tile<D, NW>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
-    if constexpr (RC) {
-      char* rcs = st + 4 * TE + (wave < 2 ? wave * 256 : 512);
-      dma_rowc(wave == 1 ? r1 : r0, rcs, tok0, lane);
+    const int tok0 = t * TR;
+    dma_tile<D, NW, TR>(ra, st, tok0, n, tsa, wave, lane);
+    dma_tile<D, NW, TR>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
+    if constexpr (RC) {  // waves < NRC stage the constants, the others a throw-away copy
+      // (every wave issues the same number of DMAs, so one vmcnt fits all)
+      const bool real = wave < NRC;
+      const int stream = real ? wave / (TR / 64) : 0, part = real ? wave % (TR / 64) : 0;
+      char* rcs = st + 4 * TE + (real ? (stream * TR + part * 64) * 4 : 2 * TR * 4);
+      dma_rowc(stream ? r1 : r0, rcs, tok0 + part * 64, lane);
     }
   };
-  auto blk = [&](int bi) {
-    const char* st = smem + ((bi >> 1) & (NST - 1)) * STAGE_BYTES;
+  auto blk = [&](int bi) {  // bi = -1: the last block of tile -1 (the zeroed stage NST-1)
+    const char* st = smem + ((bi >> LB) & (NST - 1)) * STAGE_BYTES;
+    const float* rc = reinterpret_cast<const float*>(st + 4 * TE);
     return BlockRef<T>{reinterpret_cast<const T*>(st), reinterpret_cast<const T*>(st + TE * 2),
-                       reinterpret_cast<const float*>(st + 4 * TE), 32 * (bi & 1), bi};
+                       rc, rc + TR, 32 * (bi & (BPT - 1)), bi};
   };
   // Stage NST-1 stands in for tile -1: zeroed, so G(-1) (the previous block's products at
   // t = 0) reads zero rows and adds nothing -- the loop body needs no t > 0 branch.
@@ -585,28 +600,35 @@ __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, in
     for (int t = 0; t < ntiles; ++t) {
       vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
       issue(t + PD);
-      if constexpr (LATE) V(blk(2 * t - 1));
-      S(blk(2 * t));
-      G(blk(2 * t - 1));
-      V(blk(2 * t));
-      S(blk(2 * t + 1));
-      G(blk(2 * t));
-      if constexpr (!LATE) V(blk(2 * t + 1));
+      const int b0 = BPT * t;
+      if constexpr (LATE) V(blk(b0 - 1));
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        S(blk(b0 + j));
+        G(blk(b0 + j - 1));
+        if (!LATE || j < BPT - 1) V(blk(b0 + j));
+      }
       if constexpr (SCH::on && !LATE) {
-        SCH::emit();
-        SCH::emit();
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) SCH::emit();
       }
     }
-    if constexpr (LATE) V(blk(2 * ntiles - 1));
-    G(blk(2 * ntiles - 1));
+    if constexpr (LATE) V(blk(BPT * ntiles - 1));
+    G(blk(BPT * ntiles - 1));
   };
   if (late) run(std::true_type{});
   else run(std::false_type{});
   vm_drain();
 }
 
-template <int D, bool RC>
-constexpr size_t tile_pipe_lds() { return 4 * (size_t)(2 * kTile * D * 2 + (RC ? 768 : 0)); }
+template <int D, bool RC, int TR = kTile>
+constexpr size_t tile_pipe_lds() { return 4 * (size_t)pipe_stage_bytes<D, RC, TR>(); }
+
+// Tile rows of the 8-wave head_dim-64 pipelined backward kernels (A/B: -DVD_PIPE_TR=128).
+#ifndef VD_PIPE_TR
+#define VD_PIPE_TR 64
+#endif
+template <int D, int NW> constexpr int pipe_tr() { return D == 64 && NW == 8 ? VD_PIPE_TR : kTile; }
 
 
 template <typename T, int D, bool RC>
@@ -1208,7 +1230,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
   for (int i = 0; i < D / 32; ++i) acc[i] = f32x16{};
   XOp<T> ds{};
 
-  tile_pipe<T, D, false, NW, typename std::conditional<kSchedOn, DqSched<D>, NoSched>::type>(
+  tile_pipe<T, D, false, NW, typename std::conditional<kSchedOn, DqSched<D>, NoSched>::type,
+            pipe_tr<D, NW>()>(
       smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
       [&](const BlockRef<T>& bs) {
         s = il;
@@ -1250,7 +1273,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   for (int i = 0; i < D / 32; ++i) adv[i] = adk[i] = f32x16{};
   XOp<T> pp{}, ds{};
 
-  tile_pipe<T, D, true, NW, typename std::conditional<kSchedOn, DkdvSched<D>, NoSched>::type>(
+  tile_pipe<T, D, true, NW, typename std::conditional<kSchedOn, DkdvSched<D>, NoSched>::type,
+            pipe_tr<D, NW>()>(
       smem, q + base, dout + obase, ts, ots, nlse2 + (int64_t)seq * n, ndelta + (int64_t)seq * n,
       n, tid, late,
       [&](const BlockRef<T>& bs) {
@@ -1258,7 +1282,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 ls = *reinterpret_cast<const float4*>(bs.rc + bs.row0 + 8 * g + 4 * hh);
-          const float4 dl = *reinterpret_cast<const float4*>(bs.rc + 64 + bs.row0 + 8 * g + 4 * hh);
+          const float4 dl = *reinterpret_cast<const float4*>(bs.rc1 + bs.row0 + 8 * g + 4 * hh);
           s[4 * g + 0] = ls.x; s[4 * g + 1] = ls.y; s[4 * g + 2] = ls.z; s[4 * g + 3] = ls.w;
           dp[4 * g + 0] = dl.x; dp[4 * g + 1] = dl.y; dp[4 * g + 2] = dl.z; dp[4 * g + 3] = dl.w;
         }
@@ -1462,7 +1486,7 @@ int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
                    hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
-  const size_t lds = tile_pipe_lds<D, false>();
+  const size_t lds = tile_pipe_lds<D, false, pipe_tr<D, NW>()>();
   auto kern = attn_bwd_dq_pipe_kernel<T, D, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
@@ -1529,7 +1553,7 @@ int dkdv_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const 
                      hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
-  const size_t lds = tile_pipe_lds<D, true>();
+  const size_t lds = tile_pipe_lds<D, true, pipe_tr<D, NW>()>();
   auto kern = attn_bwd_dkdv_pipe_kernel<T, D, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
