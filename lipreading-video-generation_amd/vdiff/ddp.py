@@ -18,14 +18,25 @@ import torch
 import torch.distributed as dist
 
 
+def local_device_index(local: int) -> int:
+    """GPU of a local rank: one per GPU.  More local ranks than GPUs (a multi-rank rehearsal
+    on a one-GPU box, VDIFF_DIST_BACKEND=gloo) share the GPUs round-robin."""
+    count = torch.cuda.device_count()  # does not initialise the GPU
+    return local % count if count > 0 else local
+
+
 def init_from_env(backend: str | None = None):
-    """Initialise the default process group from torchrun's env; returns (rank, world, local)."""
+    """Initialise the default process group from torchrun's env; returns (rank, world, local).
+
+    backend: None = VDIFF_DIST_BACKEND if set, else "nccl" (RCCL) with a GPU, else "gloo".
+    `local` is the GPU index (local_device_index), not necessarily LOCAL_RANK."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device_index(int(os.environ.get("LOCAL_RANK", "0")))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("VDIFF_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(local)
@@ -41,7 +52,7 @@ class _Bucket:
     def __init__(self, params, flat):
         self.params = params
         self.flat = flat
-        self.pending = len(params)
+        self.pending = len(params)  # parameters still without this step's gradient
         self.work = None
         self.launched = False
 
@@ -52,6 +63,13 @@ class GradBucketer:
     Usage per step:  loss.backward(); bucketer.finish(); optimizer.step();
     bucketer.zero_grad()  (never optimizer.zero_grad(set_to_none=True): p.grad must
     stay a view of the bucket buffer).
+
+    Buckets are launched strictly in bucket order on every rank: a ready bucket waits for
+    its predecessors.  Which parameters receive a gradient can differ between ranks
+    (wav2vec2's LayerDrop and SpecAugment in train mode skip layers / the mask embedding at
+    random), so launching in hook-completion order would pair different buckets in one
+    collective.  A bucket with a parameter that got no gradient launches from finish(),
+    carrying zeros for it -- what DDP's find_unused_parameters does.
     """
 
     def __init__(self, params, bucket_mb: float = 25.0, group=None):
@@ -70,6 +88,7 @@ class GradBucketer:
             size += nbytes
         if cur:
             self.buckets.append(self._make(cur))
+        self.next = 0  # first bucket not yet launched
         self.bucket_of = {}
         for b in self.buckets:
             for p in b.params:
@@ -93,18 +112,19 @@ class GradBucketer:
         b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _hook(self, p):
-        b = self.bucket_of[p]
-        b.pending -= 1
-        if b.pending == 0 and not b.launched:
-            self._launch(b)
+        self.bucket_of[p].pending -= 1
+        while self.next < len(self.buckets) and self.buckets[self.next].pending == 0:
+            self._launch(self.buckets[self.next])
+            self.next += 1
 
     def finish(self):
-        """Wait for every bucket (launching any whose params got no gradient) and average."""
+        """Launch the remaining buckets in order (those with parameters that got no
+        gradient, and their successors), wait for all, and average."""
         if self.world == 1:
             return
-        for b in self.buckets:
-            if not b.launched:
-                self._launch(b)
+        for b in self.buckets[self.next:]:
+            self._launch(b)
+        self.next = len(self.buckets)
         for b in self.buckets:
             b.work.wait()
             b.flat.mul_(1.0 / self.world)
@@ -115,6 +135,7 @@ class GradBucketer:
             b.flat.zero_()
             b.pending = len(b.params)
             b.launched = False
+        self.next = 0
 
     @property
     def nbytes(self):

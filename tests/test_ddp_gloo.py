@@ -74,3 +74,74 @@ def test_bucketed_allreduce_matches_single_process():
     torch.nn.functional.mse_loss(m(x), y).backward()
     for g, p in zip(got, m.parameters()):
         torch.testing.assert_close(g, p.grad, atol=1e-6, rtol=1e-5)
+
+
+class _Skippy(torch.nn.Module):
+    """A trunk with blocks a rank may skip (as wav2vec2's LayerDrop does in train mode)."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.inp = torch.nn.Linear(16, 32)
+        self.blocks = torch.nn.ModuleList(torch.nn.Linear(32, 32) for _ in range(3))
+        self.out = torch.nn.Linear(32, 4)
+
+    def forward(self, x, skip):
+        h = torch.tanh(self.inp(x))
+        for i, b in enumerate(self.blocks):
+            if i not in skip:
+                h = h + torch.tanh(b(h))
+        return self.out(h)
+
+
+_SKIPS = {0: (1,), 1: ()}  # rank 0 drops block 1: its bucket completes on rank 1 only
+
+
+def _skippy_loss(m, rank, world):
+    x, y = _data()
+    n = x.shape[0] // world
+    return torch.nn.functional.mse_loss(m(x[rank * n:(rank + 1) * n], _SKIPS[rank]),
+                                        y[rank * n:(rank + 1) * n])
+
+
+def _skip_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from vdiff.ddp import GradBucketer, init_from_env
+    init_from_env("gloo")
+    m = _Skippy()
+    bk = GradBucketer(list(m.parameters()), bucket_mb=0.003)  # one bucket per layer or less
+    for step in range(2):
+        _skippy_loss(m, rank, world).backward()
+        bk.finish()
+        if step == 0:
+            bk.zero_grad()
+    if rank == 0:
+        out.put([p.grad.clone() for p in m.parameters()] + [torch.tensor(len(bk.buckets))])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucket_order_survives_rank_dependent_unused_params():
+    """Rank-dependent unused parameters must not reorder the collectives: buckets launch in
+    bucket order on every rank, and a skipped parameter contributes zeros to the average."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_skip_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert int(got.pop()) >= 4
+    grads = []
+    for r in range(world):
+        m = _Skippy()
+        _skippy_loss(m, r, world).backward()
+        grads.append([p.grad if p.grad is not None else torch.zeros_like(p)
+                      for p in m.parameters()])
+    for i, g in enumerate(got):
+        torch.testing.assert_close(g, sum(gr[i] for gr in grads) / world, atol=1e-6, rtol=1e-5)
