@@ -1198,6 +1198,262 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
   if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m + log2f(lt)) / kLog2e;
 }
 
+// Forward with the lagged-max check deferred to the tile boundary, so the loop body is one
+// basic block.  PV runs one tile (two 32-key blocks) behind the softmax: the check of tile
+// t-1's blocks opens tile t, before their PV; on the rare path it recomputes both blocks
+// from the still-resident K tile against their true max and rescales O and l, which then
+// hold exactly the blocks before them.  Order per tile (waves 0-3 of 8, or all waves
+// without STAGGER): [check(t-1)] S(2t) G(2t-2) V(2t) S(2t+1) G(2t-1) V(2t+1);
+// staggered waves 4-7: V(2t-1) [check(t-1)] S(2t) G(2t-2) V(2t) S(2t+1) G(2t-1).
+// Same ring as tile_pipe (4 stages, prefetch distance 2): tile t-1 stays resident while
+// t+1 and t+2 land.  bf16, D = 64 (the issue-bound shape).
+#ifndef VD_DEFER_PRE
+#define VD_DEFER_PRE 0
+#endif
+// VD_DEFER_MSUM=1: row sums on the matrix pipe (below).  Correct, but measured 22.1 vs
+// 18.0 ms at N = 262144: the 16x16x32 sum MFMAs sit on the exp -> cvt -> MFMA chain and
+// serialise on their accumulator.  Kept as an A/B build flag; off.
+#ifndef VD_DEFER_MSUM
+#define VD_DEFER_MSUM 0
+#endif
+template <typename T, int D, int NW, bool STAGGER>
+__global__ __launch_bounds__(64 * NW, 1) void attn_fwd_defer_kernel(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
+    float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
+  static_assert(kDMA<T> && D == 64, "deferred-check forward: bf16, D = 64");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TE = kTile * D, NST = 4, PD = 2;
+  constexpr int STAGE_BYTES = pipe_stage_bytes<D, false, kTile>();
+  constexpr int PER_TILE = 2 * dma_ipw<D, NW, kTile>();
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
+  const int seq = blockIdx.y;
+  const int q0 = blockIdx.x * (32 * NW) + wave * 32;
+  const int64_t base = qa(seq);
+  const bool late = STAGGER && wave >= NW / 2;
+  const int ntiles = (n + kTile - 1) / kTile;
+
+  RowFrag<T, D> qf;
+  qf.load(q + base, ts, q0 + (lane & 31), n, lane);
+  qf.scale(scale * kLog2e);
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
+  float m = -INFINITY;
+#if VD_DEFER_MSUM
+  // Row sums on the matrix pipe instead of 32 v_add per tile: a 16x16x32 MFMA with a 0/1
+  // selector as A and a block's P^T register as B.  As a 16x16x32 B operand, lane l of P^T
+  // (query l % 32) lands in column l % 16, k-group l / 16; selector row 0 takes k-groups
+  // 0 and 2 (queries 0-15), row 1 k-groups 1 and 3 (queries 16-31).  So lanes 0-15 hold
+  // the sums of query n in [0] and of query n + 16 in [1] (the bf16 P that PV uses).
+  const short one = (lane == 0 || lane == 32 || lane == 17 || lane == 49) ? (short)0x3F80 : 0;
+  const bf16x8 sel = bf16x8{one, one, one, one, one, one, one, one};
+  f32x4 lsum = f32x4{}, tsum = f32x4{};  // running / pending-tile row sums
+  auto V_sum = [&](const XOp<T>& p) __attribute__((always_inline)) {
+    tsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, p.b[0], tsum, 0, 0, 0);
+    tsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, p.b[1], tsum, 0, 0, 0);
+  };
+#else
+  float l = 0.f, psa = 0.f, psb = 0.f;
+#endif
+  f32x16 negm, sa, sb;
+  XOp<T> pa{}, pb{};  // zero: G(-2), G(-1) add nothing
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    negm[r] = INFINITY;  // m = -inf: the first tile's sums are inf -> rare path sets m
+    sb[r] = -INFINITY;   // a staggered wave's V(-1) yields p = 0, psum = 0
+  }
+
+  const auto ra = make_rsrc(k + base, seq_bytes(n, ts, D, 2));
+  const auto rb = make_rsrc(v + base, seq_bytes(n, ts, D, 2));
+  const uint32_t tsb = (uint32_t)(ts * 2);
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    char* st = smem + (t % NST) * STAGE_BYTES;
+    dma_tile<D, NW>(ra, st, t * kTile, n, tsb, wave, lane);
+    dma_tile<D, NW>(rb, st + TE * 2, t * kTile, n, tsb, wave, lane);
+  };
+  // block bi: rows [32 (bi & 1), +32) of tile bi >> 1 (bi < 0: the zeroed stage NST-1)
+  auto kblk = [&](int bi) __attribute__((always_inline)) {
+    return reinterpret_cast<const T*>(smem + ((bi >> 1) & (NST - 1)) * STAGE_BYTES);
+  };
+  auto vblk = [&](int bi) __attribute__((always_inline)) { return kblk(bi) + TE; };
+  auto mask = [&](f32x16& s, int bi) __attribute__((always_inline)) {
+    const int key0 = 32 * bi;
+    if (key0 + 32 > n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (key0 + acc_row(r, hh) >= n) s[r] = -INFINITY;
+  };
+  auto S = [&](f32x16& s, int bi) __attribute__((always_inline)) {
+    s = negm;
+    mma_rows<T, D>(s, kblk(bi), 32 * (bi & 1), qf, lane);
+  };
+  auto G = [&](const XOp<T>& p, int bi) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], vblk(bi), 32 * (bi & 1), 32 * i, p, lane);
+  };
+  // MK: the block may hold keys >= n (only the last tile's blocks can)
+#if VD_DEFER_MSUM
+  auto V = [&](f32x16& s, XOp<T>& p, float&, int bi, auto mk) __attribute__((always_inline)) {
+    if constexpr (decltype(mk)::value) mask(s, bi);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = fast_exp2(s[r]);
+    p = XOp<T>(s);
+    V_sum(p);
+  };
+  float psa = 0.f, psb = 0.f;  // unused (sums on the matrix pipe)
+#else
+  auto V = [&](f32x16& s, XOp<T>& p, float& ps, int bi, auto mk) __attribute__((always_inline)) {
+    if constexpr (decltype(mk)::value) mask(s, bi);
+    ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = fast_exp2(s[r]);
+      ps += s[r];
+    }
+    p = XOp<T>(s);
+  };
+#endif
+  // blocks 2tp, 2tp+1 hold p against the current m; their PV has not run yet
+  auto check = [&](int tp) __attribute__((always_inline)) {
+#if VD_DEFER_MSUM
+    const bool ok = lane >= 16 || (tsum[0] < kLagSum && tsum[1] < kLagSum);
+#else
+    const bool ok = psa < kLagSum && psb < kLagSum;
+#endif
+    if (!__all(ok)) {  // rare: true max of the tile
+      f32x16 s0 = f32x16{}, s1 = f32x16{};
+      mma_rows<T, D>(s0, kblk(2 * tp), 0, qf, lane);
+      mma_rows<T, D>(s1, kblk(2 * tp + 1), 32, qf, lane);
+      mask(s0, 2 * tp);
+      mask(s1, 2 * tp + 1);
+      float tmax = fmaxf(s0[0], s1[0]);
+#pragma unroll
+      for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(s0[r], s1[r]));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = fast_exp2(m - mnew);  // m = -inf: 0 (O and l are 0 then)
+      m = mnew;
+#if VD_DEFER_MSUM
+      // lanes 0-15 hold query n in [0] and query n + 16 in [1]: the latter's alpha is on
+      // lane n + 16
+      const float alpha1 = __shfl(alpha, (lane & 15) + 16, 64);
+      lsum[0] *= alpha;
+      lsum[1] *= alpha1;
+      tsum = f32x4{};
+#else
+      l *= alpha;
+#endif
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        negm[r] = -mnew;
+        s0[r] -= mnew;
+        s1[r] -= mnew;
+      }
+      V(s0, pa, psa, 2 * tp, std::false_type{});  // masked above
+      V(s1, pb, psb, 2 * tp + 1, std::false_type{});
+    }
+#if VD_DEFER_MSUM
+    lsum += tsum;
+    tsum = f32x4{};
+#else
+    l += psa + psb;
+#endif
+  };
+
+  {  // zero the stage that stands in for tile -1
+    uint4* z = reinterpret_cast<uint4*>(smem + (NST - 1) * STAGE_BYTES);
+    for (int i = tid; i < STAGE_BYTES / 16; i += 64 * NW) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  vm_drain();
+#pragma unroll
+  for (int s = 0; s < PD; ++s) issue(s);
+  // The last tile runs its own copy of the body, the only one that masks keys >= n: the
+  // steady-state body carries no branch besides the check at its top.
+  auto tile = [&](int t, auto late_c, auto mk) __attribute__((always_inline)) {
+    constexpr bool LATE = decltype(late_c)::value;
+    vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
+    issue(t + PD);
+    const int b0 = 2 * t;
+    if constexpr (LATE) V(sb, pb, psb, b0 - 1, std::false_type{});
+    check(t - 1);
+#if VD_DEFER_PRE
+    // every LDS fragment of the body up front (K rows of tile t, V^T of tile t-1; 64 VGPRs),
+    // so no MFMA waits on a just-issued read
+    bf16x8 kf[2][D / 16], vf[2][D / 32][2];
+    {
+      const T* Kt = kblk(b0);
+      const T* Vp = vblk(b0 - 2);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int ss = 0; ss < D / 16; ++ss)
+          kf[h][ss] = *reinterpret_cast<const bf16x8*>(
+              Kt + toff<T, D>(32 * h + (lane & 31), 16 * ss + 8 * hh));
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i) load_tr<D>(vf[h][i], Vp, 32 * h, 32 * i, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    auto Sp = [&](f32x16& s, int h) __attribute__((always_inline)) {
+      s = negm;
+#pragma unroll
+      for (int ss = 0; ss < D / 16; ++ss)
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[h][ss], qf.f[ss], s, 0, 0, 0);
+    };
+    auto Gp = [&](const XOp<T>& p, int h) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          oacc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[h][i][s2], p.b[s2], oacc[i], 0, 0, 0);
+    };
+    Sp(sa, 0);
+    Gp(pa, 0);
+    V(sa, pa, psa, b0, mk);
+    Sp(sb, 1);
+    Gp(pb, 1);
+#else
+    S(sa, b0);
+    G(pa, b0 - 2);
+    V(sa, pa, psa, b0, mk);
+    S(sb, b0 + 1);
+    G(pb, b0 - 1);
+#endif
+    if constexpr (!LATE) V(sb, pb, psb, b0 + 1, mk);
+  };
+  auto run = [&](auto late_c) __attribute__((always_inline)) {
+    constexpr bool LATE = decltype(late_c)::value;
+    for (int t = 0; t < ntiles - 1; ++t) tile(t, late_c, std::false_type{});
+    tile(ntiles - 1, late_c, std::true_type{});
+    if constexpr (LATE) V(sb, pb, psb, 2 * ntiles - 1, std::true_type{});
+    check(ntiles - 1);
+    G(pa, 2 * ntiles - 2);
+    G(pb, 2 * ntiles - 1);
+  };
+  // static priority for the second-dispatched wave half (MI355X_MICROARCH.md): measured
+  // 17.7 vs 17.9-18.0 ms at N = 262144
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (late) run(std::true_type{});
+  else run(std::false_type{});
+  vm_drain();
+
+  const int myq = q0 + (lane & 31);
+#if VD_DEFER_MSUM
+  const float l0 = __shfl(lsum[0], lane & 15, 64), l1 = __shfl(lsum[1], lane & 15, 64);
+  const float lt = (lane & 16) ? l1 : l0;
+#else
+  const float lt = l + __shfl_xor(l, 32, 64);
+#endif
+  store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, oacc, 1.f / lt, lane);
+  if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m + log2f(lt)) / kLog2e;
+}
+
 template <typename T, int D, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
@@ -1229,6 +1485,9 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) acc[i] = f32x16{};
   XOp<T> ds{};
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md): 23.3 vs 23.45 ms
+  // at N = 262144 (dK/dV measured no gain, so it stays off there)
+  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   tile_pipe<T, D, false, NW, typename std::conditional<kSchedOn, DqSched<D>, NoSched>::type,
             pipe_tr<D, NW>()>(
@@ -1333,7 +1592,9 @@ int check_attn(const vd_attn_desc* d) {
 // VDIFF_ATTN_CFG=base|nb2|w8|p8|p4 overrides the choice for A/B measurements.
 //   kP8 / kP4: the software-pipelined kernels (tile_pipe) with 8 / 4 waves (bf16, D <= 128;
 //          8 waves only at D = 64)
-enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4 };
+//   kD8 / kD8N: the deferred-check forward (attn_fwd_defer_kernel, bf16, D = 64), 8 waves
+//          with / without the staggered second half; other kernels keep their default
+enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kCfgLast = kD8N };
 
 int cfg_from_env() {
   const char* e = getenv("VDIFF_ATTN_CFG");
@@ -1343,6 +1604,8 @@ int cfg_from_env() {
   if (!strcmp(e, "p8")) return (int)kP8;
   if (!strcmp(e, "p4")) return (int)kP4;
   if (!strcmp(e, "base")) return (int)kBase;
+  if (!strcmp(e, "d8")) return (int)kD8;
+  if (!strcmp(e, "d8n")) return (int)kD8N;
   return -1;
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
@@ -1352,10 +1615,11 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   if (!bf16) return kBase;
   AttnCfg c = kBase;
   // defaults = the fastest measured (tools/attn_bench.py, MI355X):
-  //   D = 64 : fwd W8 17.2 ms, dQ P8 21.6 ms, dK/dV P8 29.1 ms (N = 262144)
+  //   D = 64 : fwd W8 17.2 ms, dQ P8 21.6 ms, dK/dV P8 29.1 ms (N = 262144); fwd D8N
+  //            (deferred check, static priority) 17.7 vs W8 17.9-18.1 on the same box
   //   D = 128: fwd NB2 2.0 ms, dQ W8 2.8 ms (P4 3.7), dK/dV base 4.7 ms (N = 65536)
-  if (env >= 0) c = (AttnCfg)env;
-  else if (D == 64) c = kind == 0 ? kW8 : kP8;
+  if (env >= 0 && !((env == kD8 || env == kD8N) && (D != 64 || kind != 0))) c = (AttnCfg)env;
+  else if (D == 64) c = kind == 0 ? kD8N : kP8;
   else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kW8 : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
@@ -1433,6 +1697,22 @@ int fwd_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const v
   return vd::check_launch("attn_fwd");
 }
 
+template <typename T, int D, int NW, bool STAGGER>
+int fwd_defer_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
+                     float* lse, hipStream_t st) {
+  const size_t lds = tile_pipe_lds<D, false>();
+  auto kern = attn_fwd_defer_kernel<T, D, NW, STAGGER>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
+                                   d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
+                                   d->token_stride,
+                                   SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
+                                   d->o_token_stride, d->scale);
+  return vd::check_launch("attn_fwd");
+}
+
 template <typename T, int D>
 int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
              float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -1442,8 +1722,11 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
       if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, q, k, v, o, lse, nullptr, 0, st);
     if constexpr (D == 64 || D == 128)
       if (c == kW8) return fwd_launch<T, D, 1, 8>(d, q, k, v, o, lse, nullptr, 0, st);
-    if constexpr (D == 64)
+    if constexpr (D == 64) {
       if (c == kP8) return fwd_pipe_launch<T, D, 8>(d, q, k, v, o, lse, st);
+      if (c == kD8) return fwd_defer_launch<T, D, 8, true>(d, q, k, v, o, lse, st);
+      if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
+    }
     if constexpr (D <= 128)
       if (c == kP4) return fwd_pipe_launch<T, D, 4>(d, q, k, v, o, lse, st);
   }
@@ -1643,7 +1926,7 @@ size_t vd_attention_fwd_workspace_size(const vd_attn_desc* d) {
 }
 
 int vd_attention_set_config(int cfg) {
-  if (cfg < -1 || cfg > (int)kP4) {
+  if (cfg < -1 || cfg > (int)kCfgLast) {
     (void)vd::fail(VD_EINVAL, "attention config %d", cfg);
     return -2;
   }
