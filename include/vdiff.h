@@ -256,6 +256,25 @@ int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k,
                           const void* v, const void* dout, const float* lse,
                           void* dk, void* dv, void* workspace, void* stream);
 
+/* ---- ViViT lipreading encoder ops (lipreading/huggingface_vivit_model.py:18-33
+ * over transformers' VivitModel: VivitLayer.layernorm_before/_after, final layernorm, VivitMLP
+ * with hidden_act "gelu_fast").
+ * vd_layernorm_fwd: rows of C contiguous elements (C % 8 == 0, C <= 2048); fp32 affine w, b;
+ * writes y and the fp32 per-row mean / rstd the backward reads.
+ * vd_layernorm_bwd: dx (overwritten), dw = sum(dy * xhat), db = sum(dy) over rows (fp32,
+ * overwritten, deterministic), through a workspace of vd_layernorm_workspace_size bytes.
+ * vd_gelu_tanh(_bwd): y = 0.5 x (1 + tanh(0.7978845608 x (1 + 0.044715 x^2))) on n elements
+ * (n % 8 == 0); bwd: dx = dy * y'(x). */
+size_t vd_layernorm_workspace_size(int rows, int C);
+int vd_layernorm_fwd(const void* x, const float* w, const float* b, void* y, float* mean,
+                     float* rstd, int rows, int C, float eps, int dtype, void* stream);
+int vd_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean,
+                     const float* rstd, void* dx, float* dw, float* db, int rows, int C,
+                     int dtype, void* workspace, size_t workspace_bytes, void* stream);
+int vd_gelu_tanh(const void* x, void* y, int64_t n, int dtype, void* stream);
+int vd_gelu_tanh_bwd(const void* x, const void* dy, void* dx, int64_t n, int dtype,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

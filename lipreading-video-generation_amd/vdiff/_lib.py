@@ -78,6 +78,12 @@ _SIGS = {
                                  _vp]),
     "vd_attention_bwd_dkdv": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp]),
+    "vd_layernorm_workspace_size": (_sz, [_i, _i]),
+    "vd_layernorm_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, C.c_float, _i, _vp]),
+    "vd_layernorm_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _sz,
+                              _vp]),
+    "vd_gelu_tanh": (_i, [_vp, _vp, _i64, _i, _vp]),
+    "vd_gelu_tanh_bwd": (_i, [_vp, _vp, _vp, _i64, _i, _vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

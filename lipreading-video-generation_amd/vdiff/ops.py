@@ -242,13 +242,84 @@ def silu(x):
     return SiLUFn.apply(x)
 
 
-def linear(x, weight, bias=None):
-    """x [..., Cin] @ weight[Cout, Cin]^T + bias on the implicit-GEMM kernel (1x1 conv)."""
+def linear(x, weight, bias=None, residual=None):
+    """x [..., Cin] @ weight[Cout, Cin]^T + bias (+ residual [..., Cout], fused into the
+    epilogue) on the implicit-GEMM kernel (1x1 conv)."""
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1], 1).contiguous()
     x2 = x2.movedim(1, -1).contiguous().movedim(-1, 1) if not is_cl(x2) else x2
-    y = conv(x2, weight.reshape(weight.shape[0], weight.shape[1], 1), bias)
+    res = None
+    if residual is not None:
+        res = residual.reshape(-1, weight.shape[0], 1).contiguous().to(x2.dtype)
+    y = conv(x2, weight.reshape(weight.shape[0], weight.shape[1], 1), bias, residual=res)
     return y.reshape(*lead, weight.shape[0])
+
+
+# ------------------------------------------------ LayerNorm / tanh GELU (ViViT encoder)
+class LayerNormFn(torch.autograd.Function):
+    """LayerNorm over the last dim (transformers VivitLayer.layernorm_before/_after):
+    vd_layernorm_fwd / vd_layernorm_bwd, fp32 statistics and affine parameters."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps: float):
+        _gpu(x, weight, bias)
+        x = x.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        w = weight.detach().float().contiguous()
+        b = bias.detach().float().contiguous()
+        _lib.call("vd_layernorm_fwd", _p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), rows, C,
+                  float(eps), _dtype(x), _stream(x))
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.wdt = (weight.dtype, bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        dy = dy.contiguous().to(x.dtype)
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dx = torch.empty_like(x)
+        dw = torch.empty(C, device=x.device, dtype=torch.float32)
+        db = torch.empty_like(dw)
+        nb = _lib.lib().vd_layernorm_workspace_size(rows, C)
+        ws = torch.empty(nb, device=x.device, dtype=torch.uint8)
+        _lib.call("vd_layernorm_bwd", _p(dy), _p(x), _p(w), _p(mean), _p(rstd), _p(dx), _p(dw),
+                  _p(db), rows, C, _dtype(x), _p(ws), nb, _stream(x))
+        return dx, dw.to(ctx.wdt[0]), db.to(ctx.wdt[1]), None
+
+
+def layer_norm(x, weight, bias, eps=1e-6):
+    return LayerNormFn.apply(x, weight, bias, float(eps))
+
+
+class GeluTanhFn(torch.autograd.Function):
+    """transformers' "gelu_fast" (VivitMLP activation): vd_gelu_tanh / vd_gelu_tanh_bwd."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _gpu(x)
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _lib.call("vd_gelu_tanh", _p(x), _p(y), x.numel(), _dtype(x), _stream(x))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous().to(x.dtype)
+        dx = torch.empty_like(x)
+        _lib.call("vd_gelu_tanh_bwd", _p(x), _p(dy), _p(dx), x.numel(), _dtype(x), _stream(x))
+        return dx
+
+
+def gelu_tanh(x):
+    return GeluTanhFn.apply(x)
 
 
 class CondConcatFn(torch.autograd.Function):

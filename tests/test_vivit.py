@@ -1,0 +1,167 @@
+"""ViViT lipreading classifier (BASELINE config 5).
+
+CPU: the oracle restatement (oracle/vivit.py) against transformers' own VivitModel
+(tests/golden/vivit.npz, tests/golden/gen_vivit_golden.py), and the drop-in module tree's
+state-dict keys against that class.  GPU (-m gpu): the libvdiff model (GEMM on the
+implicit-GEMM kernel, flash attention, layernorm.hip) against the golden vectors and the
+oracle -- fp32 within 1e-4 rel-L2, bf16 within 3e-2 -- and the LayerNorm / GELU kernels
+against torch fp32."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden
+from oracle.fixtures import rel_l2, seeded
+from oracle.vivit import gelu_fast, seeded_state, vivit_classifier, vivit_forward
+
+LAYERS, HEADS, CLASSES = 2, 8, 7
+dev = "cuda"
+
+
+def _model(layers=LAYERS, intermediate=512, classes=CLASSES, use_bf16=False):
+    from vdiff.vivit import ViViT, VivitModel, lipreading_config
+    cfg = lipreading_config(num_frames=5, num_hidden_layers=layers, intermediate_size=intermediate)
+    return ViViT(VivitModel(cfg, use_bf16=use_bf16), classes, 5)
+
+
+def _state(m, seed=11):
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    return seeded_state(shapes, seed)
+
+
+def test_oracle_matches_transformers_golden():
+    g = golden("vivit.npz")
+    m = _model()
+    P = {k: v.requires_grad_(True) for k, v in _state(m).items()}
+    hs = vivit_forward({k[4:]: v for k, v in P.items() if k.startswith("vit.")}, g["x"], HEADS, LAYERS)
+    assert rel_l2(hs, g["last_hidden"]) < 1e-5
+    logits = vivit_classifier(P, g["x"], HEADS, LAYERS)
+    assert rel_l2(logits, g["logits"]) < 1e-5
+    loss = F.cross_entropy(logits, g["labels"])
+    assert abs(float(loss.detach()) - float(g["loss"])) < 1e-5
+    loss.backward()
+    for k in g:
+        if k.startswith("grad_"):
+            name = k[5:]
+            assert rel_l2(P[name].grad[:8], g[k]) < 1e-4, name
+
+
+def test_state_dict_keys_match_transformers():
+    transformers = pytest.importorskip("transformers")
+    from vdiff.vivit import VivitModel, lipreading_config
+    hf = transformers.VivitModel(transformers.VivitConfig(
+        image_size=32, num_frames=5, num_channels=1, hidden_size=256, num_attention_heads=8,
+        num_hidden_layers=2))
+    ours = VivitModel(lipreading_config(num_hidden_layers=2))
+    a = {k: tuple(v.shape) for k, v in hf.state_dict().items()}
+    b = {k: tuple(v.shape) for k, v in ours.state_dict().items()}
+    assert a == b
+
+
+def test_flop_model():
+    from vdiff.vivit import lipreading_config, vivit_flops
+    cfg = lipreading_config(num_frames=5)
+    # 8 tubelets + CLS, 12 layers: patch GEMM + per layer 4 C^2 + 2 C I GEMMs + 2 N^2 C attention
+    N, C, I = 9, 256, 3072
+    want = 2 * 8 * 256 * 512 + 12 * (2 * N * (4 * C * C + 2 * C * I) + 4 * N * N * C)
+    assert vivit_flops(cfg, 1) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 3e-2)])
+def test_vivit_matches_golden(dtype, tol):
+    g = golden("vivit.npz")
+    m = _model(use_bf16=dtype == torch.bfloat16)
+    m.load_state_dict(_state(m))
+    m = m.to(dev)
+    logits = m(g["x"].to(dev))
+    assert rel_l2(logits, g["logits"]) < tol
+    hs = m.vit(g["x"].to(dev)).last_hidden_state
+    assert rel_l2(hs.float(), g["last_hidden"]) < tol
+    loss = F.cross_entropy(logits, g["labels"].to(dev))
+    loss.backward()
+    named = dict(m.named_parameters())
+    for k in g:
+        if k.startswith("grad_"):
+            name = k[5:]
+            assert rel_l2(named[name].grad[:8], g[k]) < (3 * tol if dtype != torch.float32 else tol), name
+
+
+@pytest.mark.gpu
+def test_vivit_config5_shape_vs_oracle():
+    """The full BASELINE config-5 model (12 layers, intermediate 3072, batch 16), fp32."""
+    m = _model(layers=12, intermediate=3072, classes=40)
+    P = _state(m, 3)
+    m.load_state_dict(P)
+    m = m.to(dev)
+    x = seeded((16, 5, 1, 32, 32), 9)
+    out = m(x.to(dev))
+    ref = vivit_classifier(P, x, HEADS, 12)
+    assert rel_l2(out, ref) < 1e-4
+
+
+@pytest.mark.gpu
+def test_vivit_train_step_and_pooler():
+    from vdiff.vivit import VivitTrainer
+    m = _model(use_bf16=True)
+    m.load_state_dict(_state(m))
+    m = m.to(dev)
+    tr = VivitTrainer(m)
+    x = seeded((16, 5, 1, 32, 32), 4).to(dev)
+    y = torch.randint(0, CLASSES, (16,), device=dev)
+    losses = [float(tr.step(x, y)) for _ in range(8)]
+    assert all(map(lambda v: v == v, losses)) and losses[-1] < losses[0]
+    tr.epoch_end()
+    tr.epoch_end()
+    assert abs(tr.opt.param_groups[0]["lr"] - 1e-4 * 0.2) < 1e-12  # StepLR(2, 0.2)
+    pooled = m.vit(x).pooler_output
+    assert pooled.shape == (16, 256) and torch.isfinite(pooled.float()).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,C", [(1, 8), (37, 256), (200, 768), (130, 2048)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_kernel(rows, C, dtype):
+    from vdiff import ops
+    x = (seeded((rows, C), 1) * 3 + 0.5).to(dtype)
+    w = (1 + 0.1 * seeded((C,), 2)).requires_grad_(True)
+    b = (0.1 * seeded((C,), 3)).requires_grad_(True)
+    dy = seeded((rows, C), 4).to(dtype)
+    xd = x.to(dev).requires_grad_(True)
+    wd = w.detach().to(dev).requires_grad_(True)
+    bd = b.detach().to(dev).requires_grad_(True)
+    y = ops.layer_norm(xd, wd, bd, 1e-6)
+    y.backward(dy.to(dev))
+    xr = x.float().requires_grad_(True)
+    yr = F.layer_norm(xr, (C,), w, b, 1e-6)
+    yr.backward(dy.float())
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    assert rel_l2(y, yr) < tol
+    assert rel_l2(xd.grad, xr.grad) < (2e-5 if dtype == torch.float32 else 2e-2)
+    assert rel_l2(wd.grad, w.grad) < (2e-5 if dtype == torch.float32 else 1e-2)
+    assert rel_l2(bd.grad, b.grad) < (2e-6 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gelu_tanh_kernel(dtype):
+    from vdiff import ops
+    x = (seeded((33, 512), 5) * 3).to(dtype)
+    dy = seeded((33, 512), 6).to(dtype)
+    xd = x.to(dev).requires_grad_(True)
+    y = ops.gelu_tanh(xd)
+    y.backward(dy.to(dev))
+    xr = x.float().requires_grad_(True)
+    yr = gelu_fast(xr)
+    yr.backward(dy.float())
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    assert rel_l2(y, yr) < tol
+    assert rel_l2(xd.grad, xr.grad) < tol
+
+
+@pytest.mark.gpu
+def test_layernorm_rejects_bad_width():
+    from vdiff import ops
+    with pytest.raises(RuntimeError):
+        ops.layer_norm(torch.zeros(4, 12, device=dev), torch.ones(12, device=dev),
+                       torch.zeros(12, device=dev))
