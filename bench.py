@@ -61,7 +61,12 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-size", type=int, default=32)
     ap.add_argument("--cpu-frames", type=int, default=8)
-    ap.add_argument("--only", choices=["train", "ddim", "all"], default="all")
+    ap.add_argument("--only", choices=["train", "ddim", "vivit", "all"], default="all")
+    ap.add_argument("--vivit-steps", type=int, default=20,
+                    help="timed ViViT fine-tune steps (BASELINE config 5); 0 skips the leg")
+    ap.add_argument("--vivit-batch", type=int, default=16, help="clips per GPU (reference: 16)")
+    ap.add_argument("--vivit-eager", action="store_true",
+                    help="no HIP-graph capture of the ViViT step (always eager for N > 1)")
     ap.add_argument("--c4-steps", type=int, default=1,
                     help="timed DDIM steps at BASELINE config 4 (256x256x25); 0 skips the leg")
     return ap.parse_args()
@@ -192,6 +197,47 @@ def cpu_baseline(args, target_frames_flops):
                        f"{sample_fps:.3f} frames/s measured over {n} steps ({el:.1f} s), "
                        f"scaled by algorithmic fwd FLOP/frame "
                        f"{f_sample / 1e9:.1f} GF -> {target_frames_flops / 1e9:.1f} GF")}
+
+
+def vivit_leg(args, rank, world, device):
+    """BASELINE config 5: ViViT lipreading fine-tune step (huggingface_vivit_model.py:35-60:
+    CE + AdamW 1e-4, batch 16 per GPU, 5x1x32x32 clips, main.py:57 config with 5 frames),
+    DDP over the same gradient bucketer; bf16 activations, fp32 master weights."""
+    from vdiff.ddp import broadcast_parameters
+    from vdiff.vivit import ViViT, VivitModel, VivitTrainer, lipreading_config, vivit_flops
+    cfg = lipreading_config(num_frames=5)
+    torch.manual_seed(4321)
+    model = ViViT(VivitModel(cfg, use_bf16=args.dtype == "bf16"), 40, 5).to(device)
+    broadcast_parameters(model)
+    graph = world == 1 and not args.vivit_eager
+    tr = VivitTrainer(model, graph=graph)
+    g = torch.Generator(device=device).manual_seed(300 + rank)
+    B = args.vivit_batch
+    x = torch.randn((B, 5, 1, 32, 32), generator=g, device=device)
+    y = torch.randint(0, 40, (B,), generator=g, device=device)
+    for _ in range(3):
+        tr.step(x, y)
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(args.vivit_steps):
+        loss = tr.step(x, y)
+    barrier_sync(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, device)
+    ms = el / args.vivit_steps * 1e3
+    flop = 3 * vivit_flops(cfg, B)
+    out = {"metric": "ViViT lipreading fine-tune clips/sec (BASELINE config 5)",
+           "value": round(world * B * args.vivit_steps / el, 2), "unit": "clips/s",
+           "ms_per_step": round(ms, 3), "batch_per_gpu": B, "clip": [5, 1, 32, 32],
+           "tokens": 9, "hidden": cfg.hidden_size, "layers": cfg.num_hidden_layers,
+           "heads": cfg.num_attention_heads, "train_tflop_per_step": round(flop / 1e12, 4),
+           "model_tflops_per_gpu": round(flop / (el / args.vivit_steps) / 1e12, 2),
+           "bound": "launch (9 tokens x 256 hidden: microsecond kernels)",
+           "parallelism": f"dp{world}", "loss": round(float(loss), 4),
+           "hip_graph": graph}
+    log(f"vivit: {ms:.2f} ms/step, {out['value']} clips/s")
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -327,6 +373,9 @@ def main():
             torch.cuda.empty_cache()
         if "value" not in result:
             result.update(value=ddim["value"], unit="steps/s", ms_per_step=ddim["ms_per_step"])
+
+    if args.only in ("vivit", "all") and args.vivit_steps > 0:
+        result["vivit"] = vivit_leg(args, rank, world, device)
 
     result["config"] = {
         "workload": f"train step, audio-conditioned UNet3D {args.size}x{args.size}x{args.frames} "

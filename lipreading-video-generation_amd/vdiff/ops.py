@@ -246,13 +246,13 @@ def linear(x, weight, bias=None, residual=None):
     """x [..., Cin] @ weight[Cout, Cin]^T + bias (+ residual [..., Cout], fused into the
     epilogue) on the implicit-GEMM kernel (1x1 conv)."""
     lead = x.shape[:-1]
-    x2 = x.reshape(-1, x.shape[-1], 1).contiguous()
-    x2 = x2.movedim(1, -1).contiguous().movedim(-1, 1) if not is_cl(x2) else x2
+    # the rows as the pixels of ONE channels-last 1-D image: logical [1, Cin, M]
+    x2 = x.reshape(1, -1, x.shape[-1]).contiguous().transpose(1, 2)
     res = None
     if residual is not None:
-        res = residual.reshape(-1, weight.shape[0], 1).contiguous().to(x2.dtype)
+        res = residual.reshape(1, -1, weight.shape[0]).contiguous().to(x2.dtype).transpose(1, 2)
     y = conv(x2, weight.reshape(weight.shape[0], weight.shape[1], 1), bias, residual=res)
-    return y.reshape(*lead, weight.shape[0])
+    return y.transpose(1, 2).reshape(*lead, weight.shape[0])
 
 
 # ------------------------------------------------ LayerNorm / tanh GELU (ViViT encoder)
@@ -449,11 +449,24 @@ def channel_sums(x: torch.Tensor) -> torch.Tensor:
     if Cc % 8:
         x = _pad_channels(x, (Cc + 7) // 8 * 8)
     cp = x.shape[1]
-    out = torch.empty(B, cp, dtype=torch.float32, device=x.device)
-    ws = torch.empty(_lib.lib().vd_channel_sums_workspace_size(B, cp), dtype=torch.uint8,
-                     device=x.device)
-    _lib.call("vd_channel_sums", _p(x), B, S, cp, 0, _dtype(x), _p(out), _p(ws), _stream(x))
-    return out[:, :Cc]
+    if cp <= 2048:
+        out = torch.empty(B, cp, dtype=torch.float32, device=x.device)
+        ws = torch.empty(_lib.lib().vd_channel_sums_workspace_size(B, cp), dtype=torch.uint8,
+                         device=x.device)
+        _lib.call("vd_channel_sums", _p(x), B, S, cp, 0, _dtype(x), _p(out), _p(ws), _stream(x))
+        return out[:, :Cc]
+    # wider than one pass takes (e.g. the ViViT MLP's 3072): 2048-channel slices through the
+    # channel stride
+    parts = []
+    for c0 in range(0, cp, 2048):
+        w = min(2048, cp - c0)
+        o = torch.empty(B, w, dtype=torch.float32, device=x.device)
+        ws = torch.empty(_lib.lib().vd_channel_sums_workspace_size(B, w), dtype=torch.uint8,
+                         device=x.device)
+        _lib.call("vd_channel_sums", x.data_ptr() + c0 * x.element_size(), B, S, w, cp,
+                  _dtype(x), _p(o), _p(ws), _stream(x))
+        parts.append(o)
+    return torch.cat(parts, dim=1)[:, :Cc]
 
 
 def _conv_key(Ci, Co, k, s, out):
