@@ -197,3 +197,23 @@ def test_layernorm_rejects_bad_width():
     with pytest.raises(RuntimeError):
         ops.layer_norm(torch.zeros(4, 12, device=dev), torch.ones(12, device=dev),
                        torch.zeros(12, device=dev))
+
+
+@pytest.mark.gpu
+def test_dropin_train_huggingface_model():
+    """The reference's entry point (huggingface_vivit_model.py:35-95) on a small seeded set."""
+    import importlib.util
+    import os
+    from conftest import PKG
+    spec = importlib.util.spec_from_file_location(
+        "hf_vivit_dropin", os.path.join(PKG, "lipreading", "huggingface_vivit_model.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    m = mod.ViViT(mod.VivitModel(mod.lipreading_config(num_hidden_layers=2)), 5, 5)
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(48, 5 * 32 * 32, generator=g)
+    Y = torch.randint(0, 5, (48,), generator=g)
+    logs = []
+    out = mod.train_huggingface_model(m, X[:32], Y[:32], X[32:], Y[32:], num_epochs=3,
+                                      log=logs.append)
+    assert out is m and len(logs) == 6 and "val loss" in logs[-1]
