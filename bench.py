@@ -199,6 +199,39 @@ def cpu_baseline(args, target_frames_flops):
                        f"{f_sample / 1e9:.1f} GF -> {target_frames_flops / 1e9:.1f} GF")}
 
 
+def vivit_cpu_baseline(model, B):
+    """The oracle (oracle/vivit.py, torch fp32 on the host cores) fine-tune step -- CE +
+    backward + AdamW -- on the same config-5 batch shape, with the GPU model's weights."""
+    import torch.nn.functional as F
+    from oracle.vivit import vivit_classifier
+    P = {k: v.detach().float().cpu().clone().requires_grad_(True)
+         for k, v in model.state_dict().items()}
+    opt = torch.optim.AdamW(list(P.values()), lr=1e-4)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn((B, 5, 1, 32, 32), generator=g)
+    y = torch.randint(0, 40, (B,), generator=g)
+    cfg = model.vit.config
+
+    def step():
+        loss = F.cross_entropy(vivit_classifier(P, x, cfg.num_attention_heads,
+                                                cfg.num_hidden_layers), y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+
+    step()
+    t0, n = time.perf_counter(), 0
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el > 5.0 or n >= 50:
+            break
+    return {"value": round(n * B / el, 2), "unit": "clips/s", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"oracle fp32 fine-tune step (fwd+CE+bwd+AdamW), batch {B}, "
+                                      f"{n} steps in {el:.1f} s"}
+
+
 def vivit_leg(args, rank, world, device):
     """BASELINE config 5: ViViT lipreading fine-tune step (huggingface_vivit_model.py:35-60:
     CE + AdamW 1e-4, batch 16 per GPU, 5x1x32x32 clips, main.py:57 config with 5 frames),
@@ -234,6 +267,11 @@ def vivit_leg(args, rank, world, device):
            "bound": "launch (9 tokens x 256 hidden: microsecond kernels)",
            "parallelism": f"dp{world}", "loss": round(float(loss), 4),
            "hip_graph": graph}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = vivit_cpu_baseline(model, B)
+        except Exception as e:  # never let the baseline leg kill the GPU numbers
+            out["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
     log(f"vivit: {ms:.2f} ms/step, {out['value']} clips/s")
     del tr, model
     torch.cuda.empty_cache()

@@ -64,6 +64,19 @@ def lipreading_config(num_frames: int = 5, **kw) -> VivitConfig:
     return VivitConfig(**base)
 
 
+def tubelets(pixel_values: torch.Tensor, tubelet) -> torch.Tensor:
+    """[B, T, C, H, W] -> [B, nt*nh*nw, C*t*h*w]: the non-overlapping tubelets (trailing
+    frames / pixels that do not fill one are dropped, as Conv3d with kernel = stride does),
+    each flattened in the (C, kt, kh, kw) order of the Conv3d weight, tokens in (t, h, w)
+    order as Conv3d(...).flatten(2)."""
+    B, T, C, H, W = pixel_values.shape
+    t, h, w = tubelet
+    nt, nh, nw = T // t, H // h, W // w
+    x = pixel_values[:, :nt * t, :, :nh * h, :nw * w]
+    x = x.reshape(B, nt, t, C, nh, h, nw, w).permute(0, 1, 4, 6, 3, 2, 5, 7)
+    return x.reshape(B, nt * nh * nw, C * t * h * w)
+
+
 class VivitTubeletEmbeddings(nn.Module):
     def __init__(self, config: VivitConfig):
         super().__init__()
@@ -75,14 +88,8 @@ class VivitTubeletEmbeddings(nn.Module):
                                     kernel_size=self.tubelet, stride=self.tubelet)
 
     def forward(self, pixel_values: torch.Tensor) -> torch.Tensor:
-        """[B, T, C, H, W] -> [B, patches, hidden]: the non-overlapping tubelets gathered in
-        the (C, kt, kh, kw) order of the Conv3d weight, then one GEMM."""
-        B, T, C, H, W = pixel_values.shape
-        t, h, w = self.tubelet
-        nt, nh, nw = T // t, H // h, W // w
-        x = pixel_values[:, :nt * t, :, :nh * h, :nw * w]
-        x = x.reshape(B, nt, t, C, nh, h, nw, w).permute(0, 1, 4, 6, 3, 2, 5, 7)
-        x = x.reshape(B, nt * nh * nw, C * t * h * w)
+        """[B, T, C, H, W] -> [B, patches, hidden]: the tubelet gather, then one GEMM."""
+        x = tubelets(pixel_values, self.tubelet)
         wgt = self.projection.weight.reshape(self.projection.weight.shape[0], -1)
         return ops.linear(x, wgt, self.projection.bias)
 

@@ -58,6 +58,18 @@ def test_state_dict_keys_match_transformers():
     assert a == b
 
 
+@pytest.mark.parametrize("T,C,HW", [(5, 1, 32), (4, 3, 48), (7, 2, 35)])
+def test_tubelet_gather_equals_conv3d(T, C, HW):
+    """Host-side tubelet gather: gather @ W^T + b == Conv3d(kernel = stride = tubelet)."""
+    from vdiff.vivit import tubelets
+    x = seeded((2, T, C, HW, HW), 1)
+    w = seeded((24, C, 2, 16, 16), 2)
+    b = seeded((24,), 3)
+    ref = F.conv3d(x.transpose(1, 2), w, b, stride=(2, 16, 16)).flatten(2).transpose(1, 2)
+    got = tubelets(x, (2, 16, 16)) @ w.reshape(24, -1).T + b
+    assert rel_l2(got, ref) < 1e-6
+
+
 def test_flop_model():
     from vdiff.vivit import lipreading_config, vivit_flops
     cfg = lipreading_config(num_frames=5)
