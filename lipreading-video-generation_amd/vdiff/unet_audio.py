@@ -14,6 +14,8 @@ reference computation.
 """
 from __future__ import annotations
 
+import os
+
 import warnings
 
 import torch as th
@@ -102,6 +104,12 @@ class UNetAudio(UNetModel):
                                        self.audio_transformer.transform[0].in_features):
             if self.audio_encoder is None:
                 raise ValueError("model built without an audio encoder: pass pooled features")
+            if (self.dtype == th.bfloat16 and next(self.audio_encoder.parameters()).is_cuda
+                    and not os.environ.get("VDIFF_W2V_FP32")):  # env: fp32 A/B switch
+                # bf16 throughput mode: wav2vec2's GEMMs / convs in bf16
+                # under autocast; fp32 master weights, fp32 pooled output
+                with th.autocast("cuda", dtype=th.bfloat16):
+                    return self.audio_encoder(audio).float().mean(dim=1)
             return self.audio_encoder(audio).mean(dim=1)
         return audio
 
