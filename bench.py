@@ -66,7 +66,9 @@ def parse():
                     help="timed ViViT fine-tune steps (BASELINE config 5); 0 skips the leg")
     ap.add_argument("--vivit-batch", type=int, default=16, help="clips per GPU (reference: 16)")
     ap.add_argument("--vivit-eager", action="store_true",
-                    help="no HIP-graph capture of the ViViT step (always eager for N > 1)")
+                    help="no HIP-graph capture of the ViViT step")
+    ap.add_argument("--vivit-graph-ddp", action="store_true",
+                    help="N > 1: graph-captured ViViT step around one all-reduce")
     ap.add_argument("--c4-steps", type=int, default=1,
                     help="timed DDIM steps at BASELINE config 4 (256x256x25); 0 skips the leg")
     return ap.parse_args()
@@ -242,7 +244,10 @@ def vivit_leg(args, rank, world, device):
     torch.manual_seed(4321)
     model = ViViT(VivitModel(cfg, use_bf16=args.dtype == "bf16"), 40, 5).to(device)
     broadcast_parameters(model)
-    graph = world == 1 and not args.vivit_eager
+    # one process: the whole step as one HIP graph.  N > 1: eager with the bucketed
+    # all-reduce (the path the UNet leg proves at scale) unless --vivit-graph-ddp (graph
+    # replays around one all-reduce; rehearsed over gloo only)
+    graph = not args.vivit_eager and (world == 1 or args.vivit_graph_ddp)
     tr = VivitTrainer(model, graph=graph)
     g = torch.Generator(device=device).manual_seed(300 + rank)
     B = args.vivit_batch

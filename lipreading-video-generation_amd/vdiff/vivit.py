@@ -242,21 +242,25 @@ class VivitTrainer:
     StepLR(step_size=2, gamma=0.2) as the reference does once per epoch."""
 
     def __init__(self, model: ViViT, lr=1e-4, bucket_mb=25.0, graph=False):
-        """graph=True (one process only): the whole step -- forward, backward, AdamW -- is
-        captured once into a HIP graph and replayed; at 9 tokens x 256 hidden every kernel
-        runs for microseconds, so the eager step is bound by host-side launch overhead."""
+        """graph=True: the step runs as captured HIP graphs.  At 9 tokens x 256 hidden every
+        kernel runs for microseconds, so an eager step is bound by host-side launch
+        overhead.  One process: forward, backward and AdamW in one graph.  Under DDP: graph
+        1 = forward + backward + gradient flatten into one fp32 buffer, then ONE eager
+        all-reduce of that buffer (the collective stays outside the capture), then graph 2 =
+        unflatten / average + AdamW."""
         from .ddp import GradBucketer
         self.model = model
-        params = [p for p in model.parameters() if p.requires_grad]
-        distributed = torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1
-        if graph and distributed:
-            raise ValueError("graph capture of the step is single-process only")
-        self.bucketer = GradBucketer(params, bucket_mb) if distributed else None
-        kw = {"fused": True} if params and params[0].is_cuda else {}
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.distributed = (torch.distributed.is_initialized()
+                            and torch.distributed.get_world_size() > 1)
+        self.world = torch.distributed.get_world_size() if self.distributed else 1
+        self.bucketer = (GradBucketer(self.params, bucket_mb)
+                         if self.distributed and not graph else None)
+        kw = {"fused": True} if self.params and self.params[0].is_cuda else {}
         if graph:
             kw["capturable"] = True
-            lr = torch.tensor(lr, device=params[0].device)
-        self.opt = torch.optim.AdamW(params, lr=lr, **kw)
+            lr = torch.tensor(lr, device=self.params[0].device)
+        self.opt = torch.optim.AdamW(self.params, lr=lr, **kw)
         self.sched = torch.optim.lr_scheduler.StepLR(self.opt, step_size=2, gamma=0.2)
         self.use_graph = graph
         self.graph = None
@@ -269,21 +273,56 @@ class VivitTrainer:
         self.static_x.copy_(data)
         self.static_y.copy_(labels)
         self.graph.replay()
+        if self.distributed:
+            torch.distributed.all_reduce(self.flat)
+            self.graph_opt.replay()
         return self.static_loss
+
+    def _fwd_bwd(self, x, y):
+        self.model.train()
+        loss = F.cross_entropy(self.model(x), y)
+        loss.backward()
+        return loss.detach()
 
     def _capture(self, data, labels):
         self.static_x = data.clone()
         self.static_y = labels.clone()
-        side = torch.cuda.Stream(device=data.device)
-        side.wait_stream(torch.cuda.current_stream(data.device))
+        dev = data.device
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(3):  # warm the allocator and autograd outside the capture
-                self._step(self.static_x, self.static_y)
-        torch.cuda.current_stream(data.device).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
+                if self.distributed:  # identical updates on every rank: average first
+                    self._fwd_bwd(self.static_x, self.static_y)
+                    for p in self.params:
+                        if p.grad is not None:
+                            torch.distributed.all_reduce(p.grad)
+                            p.grad.div_(self.world)
+                    self.opt.step()
+                    self.opt.zero_grad(set_to_none=True)
+                else:
+                    self._step(self.static_x, self.static_y)
+        torch.cuda.current_stream(dev).wait_stream(side)
         self.opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph):
-            self.static_loss = self._step(self.static_x, self.static_y, zero=False)
+        self.graph = torch.cuda.CUDAGraph()
+        if not self.distributed:
+            with torch.cuda.graph(self.graph):
+                self.static_loss = self._step(self.static_x, self.static_y, zero=False)
+            return
+        # parameters with a gradient (the pooler has none: the classifier never reads it).
+        # thread_local: the process group's watchdog thread may query events meanwhile.
+        torch.cuda.synchronize(dev)
+        torch.distributed.barrier()
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            self.static_loss = self._fwd_bwd(self.static_x, self.static_y)
+            grads = [p.grad for p in self.params if p.grad is not None]
+            self.flat = torch.cat([g.reshape(-1).float() for g in grads])
+        self.graph_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_opt, capture_error_mode="thread_local"):
+            views = self.flat.split([g.numel() for g in grads])
+            torch._foreach_mul_(list(views), 1.0 / self.world)
+            torch._foreach_copy_(grads, [v.view_as(g) for v, g in zip(views, grads)])
+            self.opt.step()
 
     def _step(self, data, labels, zero=True):
         self.model.train()
