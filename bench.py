@@ -418,7 +418,11 @@ def main():
             result.update(value=ddim["value"], unit="steps/s", ms_per_step=ddim["ms_per_step"])
 
     if args.only in ("vivit", "all") and args.vivit_steps > 0:
-        result["vivit"] = vivit_leg(args, rank, world, device)
+        try:  # an auxiliary leg: never let it take the headline numbers down
+            result["vivit"] = vivit_leg(args, rank, world, device)
+        except Exception as e:
+            log(f"vivit leg failed: {type(e).__name__}: {e}")
+            result["vivit"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
 
     result["config"] = {
         "workload": f"train step, audio-conditioned UNet3D {args.size}x{args.size}x{args.frames} "
