@@ -1217,7 +1217,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
 #define VD_DEFER_MSUM 0
 #endif
 template <typename T, int D, int NW, bool STAGGER>
-__global__ __launch_bounds__(64 * NW, 1) void attn_fwd_defer_kernel(
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   static_assert(kDMA<T> && D == 64, "deferred-check forward: bf16, D = 64");
@@ -1594,7 +1594,10 @@ int check_attn(const vd_attn_desc* d) {
 //          8 waves only at D = 64)
 //   kD8 / kD8N: the deferred-check forward (attn_fwd_defer_kernel, bf16, D = 64), 8 waves
 //          with / without the staggered second half; other kernels keep their default
-enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kCfgLast = kD8N };
+//   kD4: the deferred-check forward with 4 waves, two workgroups per CU (the SIMD partners
+//          then come from different workgroups and share no barrier)
+enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
+               kCfgLast = kD4 };
 
 int cfg_from_env() {
   const char* e = getenv("VDIFF_ATTN_CFG");
@@ -1606,6 +1609,7 @@ int cfg_from_env() {
   if (!strcmp(e, "base")) return (int)kBase;
   if (!strcmp(e, "d8")) return (int)kD8;
   if (!strcmp(e, "d8n")) return (int)kD8N;
+  if (!strcmp(e, "d4")) return (int)kD4;
   return -1;
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
@@ -1618,7 +1622,8 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //   D = 64 : fwd W8 17.2 ms, dQ P8 21.6 ms, dK/dV P8 29.1 ms (N = 262144); fwd D8N
   //            (deferred check, static priority) 17.7 vs W8 17.9-18.1 on the same box
   //   D = 128: fwd NB2 2.0 ms, dQ W8 2.8 ms (P4 3.7), dK/dV base 4.7 ms (N = 65536)
-  if (env >= 0 && !((env == kD8 || env == kD8N) && (D != 64 || kind != 0))) c = (AttnCfg)env;
+  if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) && (D != 64 || kind != 0)))
+    c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
   else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kW8 : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
@@ -1726,6 +1731,7 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
       if (c == kP8) return fwd_pipe_launch<T, D, 8>(d, q, k, v, o, lse, st);
       if (c == kD8) return fwd_defer_launch<T, D, 8, true>(d, q, k, v, o, lse, st);
       if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
+      if (c == kD4) return fwd_defer_launch<T, D, 4, false>(d, q, k, v, o, lse, st);
     }
     if constexpr (D <= 128)
       if (c == kP4) return fwd_pipe_launch<T, D, 4>(d, q, k, v, o, lse, st);

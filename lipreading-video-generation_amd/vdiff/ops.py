@@ -722,12 +722,12 @@ class AttentionFn(torch.autograd.Function):
         return dqkv, None, None, None, None
 
 
-ATTN_CONFIGS = {"auto": -1, "base": 0, "nb2": 1, "w8": 2, "p8": 3, "p4": 4, "d8": 5, "d8n": 6}
+ATTN_CONFIGS = {"auto": -1, "base": 0, "nb2": 1, "w8": 2, "p8": 3, "p4": 4, "d8": 5, "d8n": 6, "d4": 7}
 
 
 class attention_config:
     """Context manager selecting the bf16 attention kernel shape (vd_attention_set_config):
-    "auto" (per-kernel default), "base", "nb2", "w8", "p8", "p4", "d8", "d8n".  Results agree across
+    "auto" (per-kernel default), "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4".  Results agree across
     shapes up to fp32 summation order; used by tests and A/B benchmarks."""
 
     def __init__(self, name: str):

@@ -65,7 +65,7 @@ def test_scores_with_large_logits():
     assert rel_l2(out, ref) < 2e-5
 
 
-CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n"]
+CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4"]
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
