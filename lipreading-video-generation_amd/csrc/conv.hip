@@ -226,12 +226,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
-    const int bidx = (int)(m / pix_per_b);
     const int lim = g.N - n < 8 ? g.N - n : 8;
     if (bias)
       for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
-    if (chan_add)
+    if (chan_add) {
+      const int bidx = (int)(m / pix_per_b);  // 64-bit division only where it is needed
       for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)bidx * g.N + n + e];
+    }
     T* out = dst + m * g.dNs + n;
     if (vec) {
       if (residual) {
@@ -584,12 +585,13 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_bf16_kernel(
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
-    const int bidx = (int)(m / pix_per_b);
     const int lim = g.N - n < 8 ? g.N - n : 8;
     if (bias)
       for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
-    if (chan_add)
+    if (chan_add) {
+      const int bidx = (int)(m / pix_per_b);  // 64-bit division only where it is needed
       for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)bidx * g.N + n + e];
+    }
     bf16_t* out = dst + m * g.dNs + n;
     if (vec) {
       if (residual) {
@@ -1194,12 +1196,13 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_dma_kernel(
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
-    const int bidx = (int)(m / pix_per_b);
     const int lim = g.N - n < 8 ? g.N - n : 8;
     if (bias)
       for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
-    if (chan_add)
+    if (chan_add) {
+      const int bidx = (int)(m / pix_per_b);  // 64-bit division only where it is needed
       for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)bidx * g.N + n + e];
+    }
     bf16_t* out = dst + m * g.dNs + n;
     if (vec) {
       if (residual) {
@@ -1233,9 +1236,38 @@ void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, c
                                     ca, (const bf16_t*)res);
 }
 
+// Single-K-step GEMMs (1x1 convs with Ci <= 64: qkv, proj_out, skip) are load -> MFMA ->
+// store with nothing to overlap inside a workgroup, so the tile is picked for workgroups
+// per CU: 64 x 64 (32 KB LDS, five per CU) moves 64->192 x 262144 in 95 us against 114 us
+// for the 256 x 64 tile (tools/conv1x1_bench.py).  Env VDIFF_CONV_1X1 (A/B): 0 = the
+// general tiles below, 1 = 128 x 64 (97 us), 2 = one 64 x 192 tile for N = 192 (127 us),
+// 3 = 64 x 64 (default).
+int conv_1x1_variant() {
+  static const int v = [] {
+    const char* e = getenv("VDIFF_CONV_1X1");
+    return e ? atoi(e) : 3;
+  }();
+  return v;
+}
+
 template <bool TR>
 int launch_igemm_dma(const GemmGeom& g, const void* src, const void* wt, void* dst,
                      const float* bias, const float* ca, const void* res, hipStream_t st) {
+  if (g.kt * g.kh * g.kw == 1 && g.sC <= kIgBK) {
+    const int v = conv_1x1_variant();
+    if (v == 1) {
+      launch_igd<128, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+      return VD_OK;
+    }
+    if (v == 3) {
+      launch_igd<64, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+      return VD_OK;
+    }
+    if (v == 2 && g.N > 128 && g.N <= 192) {
+      launch_igd<64, 192, 1, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+      return VD_OK;
+    }
+  }
   // two or more workgroups per CU (double-buffered ring): measured faster than one workgroup with a
   // three-stage ring on every UNet shape (tools/conv_ab4.sh).  N that is a multiple of 64 but
   // not of 128 (the qkv conv, N = 192) takes 64-wide tiles: no half-empty column tile.
