@@ -1220,7 +1220,7 @@ template <typename T, int D, int NW, bool STAGGER>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
-  static_assert(kDMA<T> && D == 64, "deferred-check forward: bf16, D = 64");
+  static_assert(kDMA<T> && (D == 64 || D == 128), "deferred-check forward: bf16, D = 64 / 128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TE = kTile * D, NST = 4, PD = 2;
   constexpr int STAGE_BYTES = pipe_stage_bytes<D, false, kTile>();
@@ -1621,11 +1621,13 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   // defaults = the fastest measured (tools/attn_bench.py, MI355X):
   //   D = 64 : fwd W8 17.2 ms, dQ P8 21.6 ms, dK/dV P8 29.1 ms (N = 262144); fwd D8N
   //            (deferred check, static priority) 17.7 vs W8 17.9-18.1 on the same box
-  //   D = 128: fwd NB2 2.0 ms, dQ W8 2.8 ms (P4 3.7), dK/dV base 4.7 ms (N = 65536)
-  if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) && (D != 64 || kind != 0)))
+  //   D = 128: fwd NB2 2.0 ms, dQ W8 2.8 ms (P4 3.7), dK/dV base 4.7 ms (N = 65536); fwd D8N
+  //            2.01 vs NB2 2.32-2.35 ms on the same box (tools/attn_ab.sh)
+  if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
+                    ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)))
     c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
-  else if (D == 128) c = kind == 0 ? kNB2 : (kind == 1 ? kW8 : kBase);
+  else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
   if (c == kP8 && D != 64) c = kP4;
@@ -1733,6 +1735,8 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
       if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
       if (c == kD4) return fwd_defer_launch<T, D, 4, false>(d, q, k, v, o, lse, st);
     }
+    if constexpr (D == 128)
+      if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
     if constexpr (D <= 128)
       if (c == kP4) return fwd_pipe_launch<T, D, 4>(d, q, k, v, o, lse, st);
   }

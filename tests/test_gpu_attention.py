@@ -97,6 +97,23 @@ def test_bf16_lagged_max_rescale(cfg):
     assert rel_l2(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("C", [64, 128])
+def test_bf16_lagged_max_rescale_default_shapes(C):
+    """The default forward (deferred check) at both head dims it serves: a key far above
+    every earlier score in a later tile, a query row with a large max, N not a multiple of
+    the 64-key tile."""
+    from vdiff import ops
+    B, N = 1, 1337
+    qkv = seeded((B, 3 * C, N), 53) * 3.0
+    qkv[:, C:2 * C, 1100] *= 12
+    qkv[:, :C, 700] *= 10
+    qkv = qkv.bfloat16().float()
+    ref = onn.qkv_attention(qkv, 1)
+    out = ops.attention(ops.to_cl(qkv.to(dev, torch.bfloat16)), heads=1)
+    assert torch.isfinite(out.float()).all()
+    assert rel_l2(out, ref) < 2e-2
+
+
 def test_config_hook_rejects_unknown():
     from vdiff import _lib, ops
     assert _lib.lib().vd_attention_set_config(9) == -2
