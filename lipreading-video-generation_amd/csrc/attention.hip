@@ -1321,7 +1321,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     const bool ok = psa < kLagSum && psb < kLagSum;
 #endif
     if (!__all(ok)) {  // rare: true max of the tile
-      f32x16 s0 = f32x16{}, s1 = f32x16{};
+      // sa / sb are dead here (their blocks' softmax ran): reuse them, no extra registers
+      f32x16& s0 = sa;
+      f32x16& s1 = sb;
+      s0 = f32x16{};
+      s1 = f32x16{};
       mma_rows<T, D>(s0, kblk(2 * tp), 0, qf, lane);
       mma_rows<T, D>(s1, kblk(2 * tp + 1), 32, qf, lane);
       mask(s0, 2 * tp);
