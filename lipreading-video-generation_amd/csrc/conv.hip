@@ -1253,7 +1253,7 @@ int conv_1x1_variant() {
 template <bool TR>
 int launch_igemm_dma(const GemmGeom& g, const void* src, const void* wt, void* dst,
                      const float* bias, const float* ca, const void* res, hipStream_t st) {
-  if (g.kt * g.kh * g.kw == 1 && g.sC <= kIgBK) {
+  if (!TR && g.kt * g.kh * g.kw == 1 && g.sC <= kIgBK) {  // forward (the measured case)
     const int v = conv_1x1_variant();
     if (v == 1) {
       launch_igd<128, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);

@@ -105,9 +105,11 @@ class UNetAudio(UNetModel):
             if self.audio_encoder is None:
                 raise ValueError("model built without an audio encoder: pass pooled features")
             if (self.dtype == th.bfloat16 and next(self.audio_encoder.parameters()).is_cuda
-                    and not os.environ.get("VDIFF_W2V_FP32")):  # env: fp32 A/B switch
-                # bf16 throughput mode: wav2vec2's GEMMs / convs in bf16
-                # under autocast; fp32 master weights, fp32 pooled output
+                    and os.environ.get("VDIFF_W2V_BF16")):
+                # opt-in bf16 wav2vec2: GEMMs / convs under autocast, fp32
+                # master weights and pooled output.  Off by default: same-box A/B of the
+                # train step measured 427-429 ms with it against 423-424 without (MIOpen's
+                # bf16 convolutions for the feature extractor are slower than its fp32 ones)
                 with th.autocast("cuda", dtype=th.bfloat16):
                     return self.audio_encoder(audio).float().mean(dim=1)
             return self.audio_encoder(audio).mean(dim=1)
