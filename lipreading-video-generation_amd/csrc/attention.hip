@@ -1102,6 +1102,10 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
 }
 
 // ================================================================== pipelined kernels
+// VD_BWD_STAGGER=0 (A/B): the 8-wave dQ / dK/dV pipelines without the staggered half
+#ifndef VD_BWD_STAGGER
+#define VD_BWD_STAGGER 1
+#endif
 #ifdef VD_ATTN_SCHED
 constexpr bool kSchedOn = true;
 #else
@@ -1468,7 +1472,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * (32 * NW) + wave * 32;
   const int64_t base = qa(seq);
-  const bool late = NW == 8 && wave >= 4;
+  const bool late = VD_BWD_STAGGER && NW == 8 && wave >= 4;
 
   RowFrag<T, D> qf, of;
   f32x16 il, id;
@@ -1525,7 +1529,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   const int seq = blockIdx.y;
   const int k0 = blockIdx.x * (32 * NW) + wave * 32;
   const int64_t base = qa(seq), obase = oa(seq);
-  const bool late = NW == 8 && wave >= 4;
+  const bool late = VD_BWD_STAGGER && NW == 8 && wave >= 4;
 
   RowFrag<T, D> kf, vf;
   kf.load(k + base, ts, k0 + (lane & 31), n, lane);
