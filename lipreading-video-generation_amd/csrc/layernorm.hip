@@ -122,7 +122,6 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(
 #pragma unroll
   for (int k = 0; k < kLnMaxChunks; ++k) {
     if (64 * k >= nch) break;  // block-uniform
-    const int c = lane + 64 * k;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       red[wave][0][8 * lane + j] = pw[k][j];
@@ -140,7 +139,6 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(
       }
     }
     __syncthreads();
-    (void)c;
   }
 }
 

@@ -21,7 +21,6 @@ takes the frame count the data has (5), which is what the reference must have me
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 from typing import Optional
 
