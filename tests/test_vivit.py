@@ -229,3 +229,28 @@ def test_dropin_train_huggingface_model():
     out = mod.train_huggingface_model(m, X[:32], Y[:32], X[32:], Y[32:], num_epochs=3,
                                       log=logs.append)
     assert out is m and len(logs) == 6 and "val loss" in logs[-1]
+
+
+def test_lipreading_dropin_names():
+    """The reference module's public names (huggingface_vivit_model.py:18, :35) import from
+    the drop-in, with the reference's signatures."""
+    import importlib.util
+    import inspect
+    import os
+    from conftest import PKG
+    spec = importlib.util.spec_from_file_location(
+        "hf_vivit_dropin_cpu", os.path.join(PKG, "lipreading", "huggingface_vivit_model.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert list(inspect.signature(mod.ViViT.__init__).parameters)[1:] == \
+        ["vivit_model", "num_classes", "num_frames"]
+    assert list(inspect.signature(mod.train_huggingface_model).parameters)[0] == "VIVIT"
+    m = mod.ViViT(mod.VivitModel(mod.lipreading_config(num_hidden_layers=1)), 9, 5)
+    assert m.fc.in_features == 256 and m.fc.out_features == 9 and m.num_frames == 5
+
+
+def test_vivit_product_path_refuses_cpu():
+    """No CPU fallback: the libvdiff ops raise on CPU tensors."""
+    m = _model(layers=1)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 5, 1, 32, 32))
