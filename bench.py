@@ -59,8 +59,9 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--ddim-steps", type=int, default=None, help="timed DDIM steps (default: --steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-size", type=int, default=32)
-    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--cpu-frames", type=int, default=2,
+                    help="frames of the bounded CPU-baseline clip (config-2 model, "
+                         "spatial_temporal)")
     ap.add_argument("--only", choices=["train", "ddim", "vivit", "all"], default="all")
     ap.add_argument("--vivit-steps", type=int, default=20,
                     help="timed ViViT fine-tune steps (BASELINE config 5); 0 skips the leg")
@@ -69,7 +70,7 @@ def parse():
                     help="no HIP-graph capture of the ViViT step")
     ap.add_argument("--vivit-graph-ddp", action="store_true",
                     help="N > 1: graph-captured ViViT step around one all-reduce")
-    ap.add_argument("--c4-steps", type=int, default=1,
+    ap.add_argument("--c4-steps", type=int, default=3,
                     help="timed DDIM steps at BASELINE config 4 (256x256x25); 0 skips the leg")
     return ap.parse_args()
 
@@ -109,96 +110,136 @@ def max_over_ranks(x, world, device):
     return float(t.item())
 
 
+def _pmc_traffic(keys):
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json),
+    summed over `keys`; None unless every key is present."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(pmc) as f:
+            tab = json.load(f)
+        vals = [tab[k].get("hbm_bytes_per_launch") for k in keys]
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if any(v is None for v in vals) else sum(vals)
+
+
 def pick_roofline(summary, dtype):
-    """Kernel with the largest total time -> roofline object + per-kernel table."""
-    from vdiff.flops import attention_kernel_flops
+    """Per-kernel executed rates, then per-UNIT algorithmic rates: unit "fwd"
+    = one forward launch (2 products); unit "bwd" = the dQ + dK/dV launch pair (4
+    products: backward = 2x forward, recompute not credited).  The roofline object is the
+    unit with the largest total time in the timed step."""
+    from vdiff.flops import attention_kernel_flops, attention_unit_flops
     peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
-    rows = []
+    rows, kern = [], {}
     for (kind, hd, n, nseq), (cnt, tot_ms) in summary.items():
         f = attention_kernel_flops(kind, n, hd, nseq)
         avg_s = tot_ms / cnt / 1e3
+        kern[(kind, hd, n, nseq)] = (cnt, tot_ms)
         rows.append({"kernel": kind, "head_dim": hd, "seq_len": n, "nseq": nseq, "launches": cnt,
                      "total_ms": round(tot_ms, 3), "avg_ms": round(tot_ms / cnt, 4),
-                     "tflop_per_launch": round(f / 1e12, 4),
-                     "tflops": round(f / avg_s / 1e12, 1),
-                     "frac": round(f / avg_s / 1e12 / peak, 4)})
+                     "executed_tflop_per_launch": round(f / 1e12, 4),
+                     "executed_tflops": round(f / avg_s / 1e12, 1),
+                     "executed_frac": round(f / avg_s / 1e12 / peak, 4)})
     rows.sort(key=lambda r: -r["total_ms"])
-    if not rows:
-        return None, rows
-    top = rows[0]
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                tab = json.load(f)
-            key = f"{top['kernel']}_d{top['head_dim']}"
-            if key in tab:
-                traffic = tab[key].get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    units = []
+    for (kind, hd, n, nseq), (cnt, tot) in kern.items():
+        if kind == "attn_fwd":
+            parts, unit = [(cnt, tot)], "fwd"
+            ex = attention_kernel_flops("attn_fwd", n, hd, nseq)
+        elif kind == "attn_bwd_dq" and ("attn_bwd_dkdv", hd, n, nseq) in kern:
+            parts, unit = [(cnt, tot), kern[("attn_bwd_dkdv", hd, n, nseq)]], "bwd"
+            ex = (attention_kernel_flops("attn_bwd_dq", n, hd, nseq)
+                  + attention_kernel_flops("attn_bwd_dkdv", n, hd, nseq))
+        else:
+            continue
+        avg_s = sum(t / c for c, t in parts) / 1e3  # one unit = one launch of each kernel
+        f = attention_unit_flops(unit, n, hd, nseq)
+        units.append({"unit": unit, "kernels": "attn_fwd" if unit == "fwd"
+                      else "attn_bwd_dq + attn_bwd_dkdv", "head_dim": hd, "seq_len": n,
+                      "nseq": nseq, "launches": parts[0][0],
+                      "total_ms": round(sum(t for _, t in parts), 3),
+                      "avg_ms": round(avg_s * 1e3, 4), "alg_tflop": round(f / 1e12, 4),
+                      "tflops": round(f / avg_s / 1e12, 1),
+                      "frac": round(f / avg_s / 1e12 / peak, 4),
+                      "executed_frac": round(ex / avg_s / 1e12 / peak, 4)})
+    units.sort(key=lambda r: -r["total_ms"])
+    if not units:
+        return None, rows, units
+    top = units[0]
+    names = ["attn_fwd"] if top["unit"] == "fwd" else ["attn_bwd_dq", "attn_bwd_dkdv"]
+    traffic = _pmc_traffic([f"{k}_d{top['head_dim']}" for k in names])
     roof = {"bound": "mfma", "achieved": top["tflops"], "peak": peak, "unit": "TFLOP/s",
-            "frac": top["frac"], "traffic": traffic,
-            "kernel": f"{top['kernel']} (head_dim {top['head_dim']}, seq {top['seq_len']}, "
+            "frac": top["frac"], "traffic": traffic, "executed_frac": top["executed_frac"],
+            "kernel": f"{top['kernels']} (head_dim {top['head_dim']}, seq {top['seq_len']}, "
                       f"{top['nseq']} seq/launch)",
-            "flop_per_launch": top["tflop_per_launch"] * 1e12, "avg_launch_ms": top["avg_ms"]}
-    return roof, rows
+            "alg_flop_per_unit": top["alg_tflop"] * 1e12, "avg_unit_ms": top["avg_ms"],
+            "note": "frac = algorithmic FLOP (SURVEY 8d: bwd = 2x fwd = 4 products, no "
+                    "recompute credit) / the unit's summed per-launch kernel time / peak; "
+                    "executed_frac counts the products the kernels run (bwd pair: 7)"}
+    return roof, rows, units
 
 
-def cpu_baseline(args, target_frames_flops):
-    """Oracle fp32 train step on a bounded sample (full-width UNet3D, joint attention,
-    reduced clip), scaled to the workload by algorithmic FLOP."""
+def _oracle_train_rate(cfg, shape, mode, audio_dim, imc_dim, budget_s, max_steps):
+    """Oracle fp32 train steps (q_sample + conditioning + fwd + MSE + bwd + Adam) at one
+    clip shape on the host cores; wav2vec2 excluded (pooled features are an input).
+    Returns (frames/s, steps, seconds)."""
     import torch.nn.functional as F
-    from oracle.fixtures import FULL3D, seeded
+    from oracle.fixtures import seeded
     from oracle.unet import (audio_conditioned_input, audio_param_shapes, build_plan,
                              init_params, param_shapes, unet_forward)
     from oracle import schedulers as osch
-    from vdiff.flops import unet_forward_work
-    from vdiff.nn import UNetModel
-
-    threads = torch.get_num_threads()
-    s, T = args.cpu_size, args.cpu_frames
-    plan = build_plan(**FULL3D)
+    B, T, s = 1, shape[0], shape[1]
+    plan = build_plan(**cfg, attention_mode=mode)
     P = init_params(param_shapes(plan), 1234)
-    P.update(init_params(audio_param_shapes(768, 128), 77))
+    P.update(init_params(audio_param_shapes(768, audio_dim, im_cond_output_ch=imc_dim), 77))
     for v in P.values():
         v.requires_grad_(True)
     tab = osch.linear_tables(100, 0.00085, 0.012)
-    x0 = seeded((1, 3, T, s, s), 0, "uniform")
-    cond = seeded((1, 3, s, s), 1, "uniform")
-    eps = seeded((1, 3, T, s, s), 2)
-    feat = seeded((T, 768), 3)
+    x0 = seeded((B, 3, T, s, s), 0, "uniform")
+    cond = seeded((B, 3, s, s), 1, "uniform")
+    eps = seeded((B, 3, T, s, s), 2)
+    feat = seeded((B * T, 768), 3)
     t = torch.tensor([37])
     opt = torch.optim.Adam(list(P.values()), lr=1e-2)
-
-    def step():
+    t0, n = time.perf_counter(), 0
+    while True:
         xt = osch.q_sample(tab, x0, eps, t)
-        x = audio_conditioned_input(P, xt, cond, feat, 128)
-        loss = F.mse_loss(unet_forward(P, plan, x, t), eps)
-        loss.backward()
+        x = audio_conditioned_input(P, xt, cond, feat, audio_dim)
+        F.mse_loss(unet_forward(P, plan, x, t), eps).backward()
         opt.step()
         opt.zero_grad()
-
-    step()  # warm
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        step()
         n += 1
         el = time.perf_counter() - t0
-        if el > 10.0 or n >= 3:
+        if el > budget_s or n >= max_steps:
             break
-    sample_fps = n * T / el
-    with torch.device("meta"):
-        m = UNetModel(image_size=s, **FULL3D)
-    f_sample = unet_forward_work(m, (1, 195, T, s, s)).total / T
-    scaled = sample_fps * f_sample / target_frames_flops
-    return {"value": scaled, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": (f"oracle fp32 train step (q_sample+fwd+MSE+bwd+Adam, wav2vec2 excluded), "
-                       f"full-width UNet3D joint attention at {s}x{s}x{T}, B=1: "
-                       f"{sample_fps:.3f} frames/s measured over {n} steps ({el:.1f} s), "
-                       f"scaled by algorithmic fwd FLOP/frame "
-                       f"{f_sample / 1e9:.1f} GF -> {target_frames_flops / 1e9:.1f} GF")}
+    return n * B * T / el, n, el
+
+
+def cpu_baseline(args):
+    """The oracle (fp32 torch-CPU restatement of the reference path) train step, measured
+    on the host cores as BASELINE.md section 3 plans -- no FLOP extrapolation:
+      * value: config 2's model (full-width UNet3D, train.py:88-97, dims=3) at 128x128 in
+        spatial_temporal mode, on a bounded 2-frame clip (per-frame work is independent of
+        T in this mode; the unit is frames/s);
+      * config1_tiny3d: BASELINE config 1 (tiny UNet3D, 64x64x8, joint attention).
+    Joint attention at 128x128x16 is n/a on a CPU: the reference materialises a 262144^2
+    fp32 score matrix (275 GB) per block."""
+    from oracle.fixtures import FULL3D, TINY3D
+    threads = torch.get_num_threads()
+    c2 = {k: v for k, v in FULL3D.items()}
+    fps2, n2, el2 = _oracle_train_rate(c2, (args.cpu_frames, args.size), "spatial_temporal",
+                                       128, 64, budget_s=8.0, max_steps=3)
+    c1 = {k: v for k, v in TINY3D.items()}
+    fps1, n1, el1 = _oracle_train_rate(c1, (8, 64), "joint", 16, 16, budget_s=8.0, max_steps=3)
+    return {"value": round(fps2, 5), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle fp32 train step (q_sample+cond+fwd+MSE+bwd+Adam, wav2vec2 "
+                       f"excluded), config-2 model (full-width UNet3D) at {args.size}x{args.size}"
+                       f", spatial_temporal attention, B=1 clip of {args.cpu_frames} frames: "
+                       f"{n2} steps in {el2:.1f} s"),
+            "joint": "n/a (262144^2 fp32 score matrix = 275 GB per block)",
+            "config1_tiny3d": {"value": round(fps1, 4), "unit": "frames/s",
+                               "sample": f"tiny UNet3D 64x64x8, joint: {n1} steps in "
+                                         f"{el1:.1f} s"}}
 
 
 def vivit_cpu_baseline(model, B):
@@ -335,8 +376,9 @@ def main():
         result["value"] = round(world * frames_per_gpu * args.steps / el, 4)
         result["ms_per_step"] = round(ms, 2)
         summary = timer.summary()
-        roof, rows = pick_roofline(summary, args.dtype)
+        roof, rows, units = pick_roofline(summary, args.dtype)
         result["roofline"] = roof
+        result["attention_units"] = units
         step_flops = 3 * work.total * args.clips_per_gpu
         result["model_tflops_per_gpu"] = round(step_flops / (el / args.steps) / 1e12, 1)
         log(f"train: {ms:.1f} ms/step, {result['value']:.3f} frames/s, loss {float(loss):.4f}, "
@@ -435,7 +477,7 @@ def main():
         result["kernels"] = rows
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            result["cpu_baseline"] = cpu_baseline(args, work.total / args.frames)
+            result["cpu_baseline"] = cpu_baseline(args)
         except Exception as e:  # never let the baseline leg kill the GPU numbers
             result["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
     else:

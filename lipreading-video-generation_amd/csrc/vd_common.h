@@ -125,14 +125,17 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 // which LDS bytes a builtin buffer_load...lds writes, so it put an s_waitcnt vmcnt(0) in
 // front of the first LDS read after it -- draining the whole ring every tile.  The ring's
 // own counted vmcnt + s_barrier (vm_wait_barrier) is what orders these writes.
+// M0 (the LDS destination) is an input operand bound with the "{m0}" constraint: the
+// compiler itself writes M0 and knows this statement reads it, so it never keeps a value
+// of its own there across the DMA.
 template <int BYTES>
 __device__ __forceinline__ void dma_lds(rsrc_t rs, uint32_t lds, uint32_t voff) {
   if constexpr (BYTES == 16)
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-                 ::"s"(lds), "v"(voff), "s"(rs));
+    asm volatile("buffer_load_dwordx4 %1, %2, 0 offen lds"
+                 ::"{m0}"(lds), "v"(voff), "s"(rs));
   else
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
-                 ::"s"(lds), "v"(voff), "s"(rs));
+    asm volatile("buffer_load_dword %1, %2, 0 offen lds"
+                 ::"{m0}"(lds), "v"(voff), "s"(rs));
 }
 
 template <int N>

@@ -3,9 +3,10 @@
 Same names: `ViViT(vivit_model, num_classes, num_frames)` (:18-33) and
 `train_huggingface_model` (:35-95).  `VivitModel` / `VivitConfig` stand in for the
 transformers classes the reference imports (:1); transformers-format state dicts load
-unchanged.  The reference's loop reads module-level X_train / Y_train / X_test / Y_test
-globals (set by main.py); here they are arguments, with the same shapes
-(N x 5 x 1 x 32 x 32 clips, integer labels).  Differences: data are moved to the GPU
+unchanged.  The reference's loop reads module-level X_train / X_test / Y_train_p /
+Y_test_p globals (set by main.py, :38-41); the one-argument call
+`train_huggingface_model(VIVIT)` does the same here, and the data may also be passed as
+arguments, with the same shapes (N x 5 x 1 x 32 x 32 clips, integer labels).  Differences: data are moved to the GPU
 once per epoch-batch as in the reference, `best_model_wts` uses copy.deepcopy (the
 reference imports `deepcopy` but calls `copy.deepcopy`, :90, a NameError), and the
 validation loss is computed rather than reusing the last training loss (:80-84).
@@ -25,10 +26,24 @@ from vdiff.vivit import (ViViT, VivitConfig, VivitModel, VivitTrainer,  # noqa: 
                          lipreading_config)
 
 
-def train_huggingface_model(VIVIT, X_train, Y_train, X_test, Y_test, num_epochs=10,
-                            batch_size=16, device="cuda", log=print):
+# module-level data the reference's one-argument call reads (:38-41); main.py sets them
+X_train = X_test = Y_train_p = Y_test_p = None
+
+
+def train_huggingface_model(VIVIT, X_train=None, Y_train=None, X_test=None, Y_test=None,
+                            num_epochs=10, batch_size=16, device="cuda", log=print):
     """huggingface_vivit_model.py:35-95: CE + AdamW(1e-4), StepLR(2, 0.2) per epoch; keeps
-    the weights of the best validation-accuracy epoch."""
+    the weights of the best validation-accuracy epoch.  Data arguments left as None are
+    read from this module's globals X_train / Y_train_p / X_test / Y_test_p, as the
+    reference does."""
+    g = globals()
+    X_train = g["X_train"] if X_train is None else X_train
+    Y_train = g["Y_train_p"] if Y_train is None else Y_train
+    X_test = g["X_test"] if X_test is None else X_test
+    Y_test = g["Y_test_p"] if Y_test is None else Y_test
+    if any(v is None for v in (X_train, Y_train, X_test, Y_test)):
+        raise NameError("train_huggingface_model: set X_train / Y_train_p / X_test / Y_test_p "
+                        "on this module (as main.py does for the reference) or pass them")
     VIVIT = VIVIT.to(device)
     X_train = torch.as_tensor(X_train).reshape(len(X_train), 5, 1, 32, 32).float()
     X_test = torch.as_tensor(X_test).reshape(len(X_test), 5, 1, 32, 32).float()

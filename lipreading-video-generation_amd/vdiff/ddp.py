@@ -69,7 +69,9 @@ class GradBucketer:
     (wav2vec2's LayerDrop and SpecAugment in train mode skip layers / the mask embedding at
     random), so launching in hook-completion order would pair different buckets in one
     collective.  A bucket with a parameter that got no gradient launches from finish(),
-    carrying zeros for it -- what DDP's find_unused_parameters does.
+    carrying zeros for it -- what DDP's find_unused_parameters does.  A parameter that got
+    no gradient on ANY rank (e.g. the ViViT pooler) has its .grad set to None for the
+    optimizer step, as in a single process, so weight decay does not touch it.
     """
 
     def __init__(self, params, bucket_mb: float = 25.0, group=None):
@@ -90,11 +92,16 @@ class GradBucketer:
             self.buckets.append(self._make(cur))
         self.next = 0  # first bucket not yet launched
         self.bucket_of = {}
+        self.index = {}  # param -> position in self.used
+        self.views = []  # (param, its gradient view into the bucket buffer)
         for b in self.buckets:
             for p in b.params:
                 self.bucket_of[p] = b
+                self.index[p] = len(self.views)
+                self.views.append((p, p.grad))
                 if self.world > 1:
                     p.register_post_accumulate_grad_hook(self._hook)
+        self.used = [0] * len(self.views)  # this rank: did the parameter get a gradient
 
     def _make(self, params):
         dev = params[0].device
@@ -112,6 +119,7 @@ class GradBucketer:
         b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _hook(self, p):
+        self.used[self.index[p]] = 1
         self.bucket_of[p].pending -= 1
         while self.next < len(self.buckets) and self.buckets[self.next].pending == 0:
             self._launch(self.buckets[self.next])
@@ -125,6 +133,20 @@ class GradBucketer:
         for b in self.buckets[self.next:]:
             self._launch(b)
         self.next = len(self.buckets)
+        used = None
+        if not all(self.used):  # some parameter got no gradient here: is it unused anywhere?
+            used = torch.tensor(self.used, dtype=torch.int32, device=self.buckets[0].flat.device)
+        flag = torch.tensor([0 if used is None else 1], dtype=torch.int32,
+                            device=self.buckets[0].flat.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        if int(flag.item()):
+            if used is None:
+                used = torch.ones(len(self.used), dtype=torch.int32,
+                                  device=self.buckets[0].flat.device)
+            dist.all_reduce(used, op=dist.ReduceOp.MAX, group=self.group)
+            for (p, _), u in zip(self.views, used.tolist()):
+                if not u:
+                    p.grad = None  # restored by zero_grad()
         for b in self.buckets:
             b.work.wait()
             b.flat.mul_(1.0 / self.world)
@@ -135,6 +157,10 @@ class GradBucketer:
             b.flat.zero_()
             b.pending = len(b.params)
             b.launched = False
+        for p, v in self.views:
+            if p.grad is None:
+                p.grad = v
+        self.used = [0] * len(self.views)
         self.next = 0
 
     @property

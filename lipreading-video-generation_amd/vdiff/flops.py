@@ -90,8 +90,18 @@ def unet_forward_work(model, x_shape) -> Work:
 
 
 def attention_kernel_flops(kind: str, n: int, ch: int, nseq: int) -> float:
-    """Algorithmic FLOP of one launch of a flash-attention kernel:
-    fwd = 2 products (QK^T, PV); bwd dQ = 3 (QK^T, dO V^T, dS K);
-    bwd dK/dV = 4 (QK^T, dO V^T, dO^T P, dS^T Q).  Each product = 2*n*n*ch per sequence."""
+    """EXECUTED FLOP of one launch of a flash-attention kernel (what the MFMAs do):
+    fwd = 2 products (QK^T, PV); bwd dQ = 3 (QK^T and dO V^T recomputed, dS K);
+    bwd dK/dV = 4 (QK^T, dO V^T, dO^T P, dS^T Q).  Each product = 2*n*n*ch per sequence.
+    The backward pair therefore executes 7 products against 4 algorithmic ones."""
     products = {"fwd": 2, "bwd_dq": 3, "bwd_dkdv": 4}[kind.replace("attn_", "")]
+    return products * 2.0 * nseq * n * n * ch
+
+
+def attention_unit_flops(unit: str, n: int, ch: int, nseq: int) -> float:
+    """ALGORITHMIC FLOP of one attention unit (backward = 2x forward, no credit
+    for recompute): unit "fwd" = 2 products (QK^T, PV); unit "bwd" = the dQ + dK/dV
+    launch pair = 4 products (dO V^T, P^T dO, dS K, dS^T Q) -- the S = QK^T each kernel
+    recomputes and the dP = dO V^T the dQ kernel recomputes are not counted."""
+    products = {"fwd": 2, "bwd": 4}[unit]
     return products * 2.0 * nseq * n * n * ch

@@ -287,6 +287,9 @@ class VivitTrainer:
         self.static_x = data.clone()
         self.static_y = labels.clone()
         dev = data.device
+        # the warm-up steps below are real updates: snapshot the weights so that the first
+        # replay is the first update the caller sees (optimizer state is reset below)
+        snapshot = [p.detach().clone() for p in self.params]
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
@@ -307,6 +310,7 @@ class VivitTrainer:
         if not self.distributed:
             with torch.cuda.graph(self.graph):
                 self.static_loss = self._step(self.static_x, self.static_y, zero=False)
+            self._restore(snapshot)
             return
         # parameters with a gradient (the pooler has none: the classifier never reads it).
         # thread_local: the process group's watchdog thread may query events meanwhile.
@@ -322,6 +326,19 @@ class VivitTrainer:
             torch._foreach_mul_(list(views), 1.0 / self.world)
             torch._foreach_copy_(grads, [v.view_as(g) for v, g in zip(views, grads)])
             self.opt.step()
+        self._restore(snapshot)
+
+    @torch.no_grad()
+    def _restore(self, snapshot):
+        """Undo the capture warm-up in place (the graphs hold these addresses): weights back
+        to the snapshot, AdamW moments and step counts to zero -- the state of a fresh
+        optimizer, so the first replay applies bias-corrected step 1."""
+        for p, v in zip(self.params, snapshot):
+            p.copy_(v)
+        for st in self.opt.state.values():
+            for v in st.values():
+                if torch.is_tensor(v):
+                    v.zero_()
 
     def _step(self, data, labels, zero=True):
         self.model.train()

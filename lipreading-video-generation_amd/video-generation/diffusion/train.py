@@ -9,7 +9,13 @@ Adam lr 1e-2, MSE on eps, batch 8, 10 epochs, state_dict saved every epoch.
 Deliberate differences: t ~ U{0..num_timesteps-1} (the reference's randint(0, 500)
 indexes a 100-entry table and crashes); one process per GPU with RCCL
 gradient all-reduce instead of a single device; --synthetic clips when the
-reference's /proj/... FrameItem pickle and decord/torchaudio stack are absent.
+reference's /proj/... FrameItem pickle and decord/torchaudio stack are absent, or
+--data <dir> for clips in the build's decoded-clip format (vdiff.data).
+Initialisation is the reference's (zero_module layers included, unet.py:222-224, 306,
+627) and wav2vec2 must load its pretrained weights (unet_audio.py:14) unless
+--random-audio-encoder (or --resume, whose checkpoint carries them) is given;
+--reinit-nonzero replaces the zero-initialised layers with seeded weights (benchmarks and
+smoke runs only).
 """
 import argparse
 import os
@@ -49,6 +55,10 @@ def parse(argv=None):
     ap.add_argument("--ckpt", default="best_diffusion.pth")
     ap.add_argument("--resume", default=None, help="checkpoint with model/optimizer/step")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--random-audio-encoder", action="store_true",
+                    help="random-init wav2vec2-base when its pretrained weights are absent")
+    ap.add_argument("--reinit-nonzero", action="store_true",
+                    help="seeded weights for the zero-initialised layers (smoke / bench only)")
     return ap.parse_args(argv)
 
 
@@ -60,7 +70,10 @@ def build_model(args):
                      channel_mult=tuple(args.channel_mult), dropout=args.dropout,
                      dims=args.dims, audio_feature_dim=768, projected_audio_dim=128,
                      use_bf16=args.dtype == "bf16", attention_mode=args.attention_mode,
-                     freeze_audio_encoder=args.freeze_audio_encoder)
+                     freeze_audio_encoder=args.freeze_audio_encoder,
+                     # True: the pretrained weights must load (raises when absent);
+                     # False: architecture only (random init, or weights from --resume)
+                     audio_encoder_pretrained=not (args.random_audio_encoder or args.resume))
 
 
 def train(argv=None):
@@ -75,7 +88,8 @@ def train(argv=None):
     scheduler = LinearNoiseScheduler(num_timesteps=args.num_timesteps, beta_start=0.00085,
                                      beta_end=0.012)
     model = build_model(args)
-    reinit_nonzero(model, seed=args.seed)
+    if args.reinit_nonzero:
+        reinit_nonzero(model, seed=args.seed)
     model = model.to(device)
     broadcast_parameters(model)
     trainer = Trainer(model, scheduler, lr=args.lr)

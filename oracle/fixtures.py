@@ -38,3 +38,23 @@ FULL2D_SHAPE = (2, 195, 32, 32)
 # train.py:88-97 / BASELINE config 2: the full-width 3-D model
 FULL3D = dict(in_channels=195, model_channels=64, out_channels=3, num_res_blocks=2,
               attention_resolutions=(1, 2, 4), channel_mult=(1, 2, 4), dims=3)
+
+
+def train_step_inputs(T=8, S=64):
+    """Seeded inputs of the one-train-step fixture (tests/golden/train_step_tiny3d.npz):
+    x0, cond image, pooled audio features [T, 64], eps."""
+    return (seeded((1, 3, T, S, S), 70, "uniform"), seeded((1, 3, 32, 32), 71, "uniform"),
+            seeded((T, 64), 72), seeded((1, 3, T, S, S), 73))
+
+
+def adam_delta_close(delta, delta_ref, grad_ref, lr=1e-2):
+    """One Adam step from zero state moves each parameter by -lr * g / (|g| + 1e-8), i.e.
+    ~ -lr * sign(g): compare where that is insensitive to the gradient's own rounding
+    (|g| above 1e-2 of its RMS: d(delta)/dg = lr * 1e-8 / (|g| + 1e-8)^2 is then <~ 1, so a
+    fp32-level gradient difference moves delta by as little), bound the rest by lr.
+    Returns the max abs deviation on the mask."""
+    delta, delta_ref, grad_ref = (u.detach().double().cpu() for u in (delta, delta_ref, grad_ref))
+    mask = grad_ref.abs() > 1e-2 * grad_ref.pow(2).mean().sqrt()
+    assert mask.float().mean() > 0.9
+    assert float(delta.abs().max()) <= lr * (1 + 1e-5)
+    return float((delta - delta_ref)[mask].abs().max())

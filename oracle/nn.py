@@ -102,16 +102,26 @@ def resblock(P, pre, x, emb, dropout_mask=None):
 
 
 def attention_block(P, pre, x, heads=1, legacy=True, mode="joint"):
-    """AttentionBlock._forward (unet.py:311-317)."""
+    """AttentionBlock._forward (unet.py:311-317).
+
+    mode "spatial_temporal" (build extension): the reference block over per-frame token
+    groups, then a second one over per-pixel groups with the temporal_* parameters."""
     B, C = x.shape[:2]
     spatial = list(x.shape[2:])
+    sp = spatial if len(spatial) == 3 else [1] + spatial
     xf = x.reshape(B, C, -1)
-    h = group_norm(xf, P[pre + "norm.weight"], P[pre + "norm.bias"])
-    qkv = conv(h, P[pre + "qkv.weight"], P[pre + "qkv.bias"])
-    a = qkv_attention(qkv, heads, legacy=legacy, mode=mode,
-                      spatial=spatial if len(spatial) == 3 else [1] + spatial)
-    h = conv(a, P[pre + "proj_out.weight"], P[pre + "proj_out.bias"])
-    return (xf + h).reshape(x.shape)
+
+    def attend(xf, pfx, md):
+        h = group_norm(xf, P[pre + pfx + "norm.weight"], P[pre + pfx + "norm.bias"])
+        qkv = conv(h, P[pre + pfx + "qkv.weight"], P[pre + pfx + "qkv.bias"])
+        a = qkv_attention(qkv, heads, legacy=legacy, mode=md, spatial=sp)
+        return xf + conv(a, P[pre + pfx + "proj_out.weight"], P[pre + pfx + "proj_out.bias"])
+
+    if mode == "spatial_temporal":
+        h = attend(attend(xf, "", "spatial"), "temporal_", "temporal")
+    else:
+        h = attend(xf, "", mode)
+    return h.reshape(x.shape)
 
 
 def upsample_block(P, pre, x, dims, use_conv=True):

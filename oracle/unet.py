@@ -20,7 +20,8 @@ from . import nn as onn
 
 def build_plan(in_channels, model_channels, out_channels, num_res_blocks, attention_resolutions,
                channel_mult=(1, 2, 4, 8), dims=2, num_heads=1, num_head_channels=-1,
-               num_heads_upsample=-1, conv_resample=True, use_new_attention_order=False):
+               num_heads_upsample=-1, conv_resample=True, use_new_attention_order=False,
+               attention_mode="joint"):
     """Layer specs per block, as UNetModel.__init__ builds them (unet.py:476-628)."""
     if num_heads_upsample == -1:
         num_heads_upsample = num_heads
@@ -61,7 +62,8 @@ def build_plan(in_channels, model_channels, out_channels, num_res_blocks, attent
             outputs.append(blk)
     return {"input_blocks": inputs, "middle_block": middle, "output_blocks": outputs,
             "model_channels": model_channels, "first_ch": first, "out_channels": out_channels,
-            "dims": dims, "legacy": not use_new_attention_order, "conv_resample": conv_resample}
+            "dims": dims, "legacy": not use_new_attention_order, "conv_resample": conv_resample,
+            "attention_mode": attention_mode}
 
 
 def _k(dims, k):
@@ -106,6 +108,13 @@ def param_shapes(plan) -> "OrderedDict[str, tuple]":
             S[pre + "qkv.bias"] = (3 * c,)
             S[pre + "proj_out.weight"] = (c, c, 1)
             S[pre + "proj_out.bias"] = (c,)
+            if plan.get("attention_mode") == "spatial_temporal":  # build extension
+                S[pre + "temporal_norm.weight"] = (c,)
+                S[pre + "temporal_norm.bias"] = (c,)
+                S[pre + "temporal_qkv.weight"] = (3 * c, c, 1)
+                S[pre + "temporal_qkv.bias"] = (3 * c,)
+                S[pre + "temporal_proj_out.weight"] = (c, c, 1)
+                S[pre + "temporal_proj_out.bias"] = (c,)
         elif kind == "down":
             S[pre + "op.weight"] = (spec[1], spec[1]) + _k(d, 3)
             S[pre + "op.bias"] = (spec[1],)
@@ -175,9 +184,10 @@ def _run_block(P, pre, blk, h, emb, plan, attn_mode):
     return h
 
 
-def unet_forward(P, plan, x, timesteps, attn_mode="joint"):
+def unet_forward(P, plan, x, timesteps, attn_mode=None):
     """UNetModel.forward (unet.py:646-675), no class conditioning."""
     mc = plan["model_channels"]
+    attn_mode = attn_mode or plan.get("attention_mode", "joint")
     e = onn.timestep_embedding(timesteps, mc)
     e = onn.linear(e, P["time_embed.0.weight"], P["time_embed.0.bias"])
     emb = onn.linear(F.silu(e), P["time_embed.2.weight"], P["time_embed.2.bias"])

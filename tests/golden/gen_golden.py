@@ -267,11 +267,65 @@ def gen_models():
     save("unet_audio2d.npz", y=y, t=torch.tensor([5, 480]))
 
 
+# ------------------------------------------------------------------ one train step
+def gen_train_step():
+    """One step of train.py:122-134 on BASELINE config 1's shape (tiny UNet3D, 64x64x8):
+    reference add_noise (q_sample) -> conditioning (unet_audio.py:52-61, restated; 5-D
+    extension D2: one reference image per clip, one pooled audio window per frame) ->
+    reference UNetModel -> MSELoss -> backward -> torch.optim.Adam(lr=1e-2).step().
+    Saves the loss and the parameter deltas of one Adam step."""
+    m = ref_unet.UNetModel(image_size=64, **TINY3D)
+    m.train()  # dropout 0 (the UNetModel default): train and eval agree
+    load_init(m, 1234)
+    A = init_params(audio_param_shapes(64, 16, im_cond_output_ch=16), 77)
+    lin = nn.Linear(64, 16)
+    lin.weight.data.copy_(A["audio_transformer.transform.0.weight"])
+    lin.bias.data.copy_(A["audio_transformer.transform.0.bias"])
+    cc = nn.Conv2d(3, 16, 1, bias=False)
+    cc.weight.data.copy_(A["cond_conv_in.weight"])
+    T, S = TINY3D_SHAPE[2], TINY3D_SHAPE[3]
+    x0 = seeded((1, 3, T, S, S), 70, "uniform")
+    cond = seeded((1, 3, 32, 32), 71, "uniform")
+    feat = seeded((T, 64), 72)
+    eps = seeded((1, 3, T, S, S), 73)
+    t = torch.tensor([37])
+    sched = ref_lns.LinearNoiseScheduler(100, 0.00085, 0.012)  # train.py:48-52
+    params = list(m.parameters()) + list(lin.parameters()) + list(cc.parameters())
+    names = [n for n, _ in m.named_parameters()] + \
+        ["audio_transformer.transform.0.weight", "audio_transformer.transform.0.bias",
+         "cond_conv_in.weight"]
+    before = [p.detach().clone() for p in params]
+    opt = torch.optim.Adam(params, 1e-2)  # train.py:102
+    opt.zero_grad()
+    xt = sched.add_noise(x0, eps, t)
+    a = F.relu(lin(feat)).reshape(1, T, 16).permute(0, 2, 1).reshape(1, 16, T, 1, 1)
+    a = a.expand(-1, -1, -1, S, S)
+    imc = cc(F.interpolate(cond, size=(S, S))).unsqueeze(2).expand(-1, -1, T, -1, -1)
+    y = m(torch.cat([xt, imc, a], dim=1), t)
+    loss = nn.MSELoss()(y, eps)
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in zip(names, params)}
+    opt.step()
+    sel = ("input_blocks.0.0.weight", "out.2.weight", "input_blocks.3.1.qkv.weight",
+           "input_blocks.3.1.proj_out.weight", "middle_block.0.in_layers.0.weight",
+           "output_blocks.0.0.skip_connection.weight", "time_embed.0.weight",
+           "audio_transformer.transform.0.weight", "cond_conv_in.weight")
+    # inputs are regenerated from their seeds by the tests (oracle.fixtures.seeded)
+    out = {"t": t, "loss": loss}
+    for n, p, b in zip(names, params, before):
+        if n in sel:
+            out["delta_" + n] = p.detach() - b
+            out["grad_" + n] = grads[n]
+    save("train_step_tiny3d.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["schedulers", "blocks", "models"]
+    which = sys.argv[1:] or ["schedulers", "blocks", "models", "train_step"]
     if "schedulers" in which:
         gen_schedulers()
     if "blocks" in which:
         gen_blocks()
     if "models" in which:
         gen_models()
+    if "train_step" in which:
+        gen_train_step()

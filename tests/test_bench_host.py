@@ -24,18 +24,33 @@ def test_attention_kernel_flops():
     assert attention_kernel_flops("attn_bwd_dkdv", n, d, 2) == pytest.approx(2 * 8 * n * n * d)
 
 
-def test_pick_roofline_takes_the_longest_kernel():
+def test_attention_unit_flops_are_algorithmic():
+    """backward = 2x forward (4 products), no credit for the recomputed S / dP."""
+    from vdiff.flops import attention_kernel_flops, attention_unit_flops
+    n, d = 262144, 64
+    assert attention_unit_flops("fwd", n, d, 1) == pytest.approx(4 * n * n * d)
+    assert attention_unit_flops("bwd", n, d, 1) == pytest.approx(8 * n * n * d)
+    executed = (attention_kernel_flops("attn_bwd_dq", n, d, 1)
+                + attention_kernel_flops("attn_bwd_dkdv", n, d, 1))
+    assert executed / attention_unit_flops("bwd", n, d, 1) == pytest.approx(7 / 4)
+
+
+def test_pick_roofline_takes_the_longest_unit():
     b = _bench()
     summary = {("attn_fwd", 64, 262144, 1): [15, 250.0],
                ("attn_bwd_dkdv", 64, 262144, 1): [15, 420.0],
+               ("attn_bwd_dq", 64, 262144, 1): [15, 300.0],
                ("attn_bwd_dq", 128, 65536, 1): [15, 37.0]}
-    roof, rows = b.pick_roofline(summary, "bf16")
-    assert [r["kernel"] for r in rows] == ["attn_bwd_dkdv", "attn_fwd", "attn_bwd_dq"]
-    f = 8 * 262144 ** 2 * 64
-    achieved = f / (420.0 / 15 / 1e3) / 1e12
-    assert roof["achieved"] == pytest.approx(achieved, rel=1e-3)
+    roof, rows, units = b.pick_roofline(summary, "bf16")
+    assert [r["kernel"] for r in rows] == ["attn_bwd_dkdv", "attn_bwd_dq", "attn_fwd",
+                                           "attn_bwd_dq"]
+    assert [u["unit"] for u in units] == ["bwd", "fwd"]  # the unpaired dQ is no unit
+    f = 8 * 262144 ** 2 * 64  # algorithmic backward: 4 products
+    t = (420.0 + 300.0) / 15 / 1e3
+    assert roof["achieved"] == pytest.approx(f / t / 1e12, rel=1e-3)
+    assert roof["frac"] == pytest.approx(f / t / 1e12 / 2500.0, rel=1e-3)
+    assert roof["executed_frac"] == pytest.approx(roof["frac"] * 7 / 4, rel=1e-3)
     assert roof["peak"] == 2500.0 and roof["unit"] == "TFLOP/s" and roof["bound"] == "mfma"
-    assert roof["frac"] == pytest.approx(achieved / 2500.0, rel=1e-3)
     assert roof["traffic"] is None or roof["traffic"] > 0
 
 

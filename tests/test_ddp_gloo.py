@@ -145,3 +145,50 @@ def test_bucket_order_survives_rank_dependent_unused_params():
                       for p in m.parameters()])
     for i, g in enumerate(got):
         torch.testing.assert_close(g, sum(gr[i] for gr in grads) / world, atol=1e-6, rtol=1e-5)
+
+
+def _global_skip_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from vdiff.ddp import GradBucketer, init_from_env
+    init_from_env("gloo")
+    m = _Skippy()
+    bk = GradBucketer(list(m.parameters()), bucket_mb=0.003)
+    skips = {0: (1, 2), 1: (2,)}  # block 2 unused on every rank, block 1 on rank 0 only
+    x, y = _data()
+    n = x.shape[0] // world
+    state = []
+    for step in range(2):
+        loss = torch.nn.functional.mse_loss(m(x[rank * n:(rank + 1) * n], skips[rank]),
+                                            y[rank * n:(rank + 1) * n])
+        loss.backward()
+        bk.finish()
+        state.append([p.grad is None for p in m.parameters()])
+        bk.zero_grad()
+    if rank == 0:
+        out.put(state + [[p.grad is None for p in m.parameters()]])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_globally_unused_params_get_no_grad():
+    """A parameter no rank produced a gradient for gets .grad = None for the optimizer step
+    (as in one process: AdamW's weight decay must not touch it); zero_grad() re-arms the
+    bucket views.  A parameter unused on one rank only keeps its (averaged) gradient."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_global_skip_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    names = [n for n, _ in _Skippy().named_parameters()]
+    for step_state in got[:2]:
+        none = {n for n, is_none in zip(names, step_state) if is_none}
+        assert none == {"blocks.2.weight", "blocks.2.bias"}, none
+    assert not any(got[2])  # after zero_grad every parameter has its bucket view again

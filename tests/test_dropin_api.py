@@ -104,3 +104,41 @@ def test_train_entry_parses_reference_defaults():
     """)
     assert json.loads(out.strip().splitlines()[-1]) == [0.01, 100, 8, 10, 64, [1, 2, 4],
                                                         [1, 2, 4], 0.1]
+
+
+def test_sampling_entry_reference_signatures():
+    """test.py keeps the reference's API: config, load_model_and_scheduler(config) and
+    sample_images(model, scheduler, img_cond, audio_cond, n_timesteps=500) (test.py:33-113),
+    importable without running the script."""
+    out = run("""
+        import json, inspect, test
+        print(json.dumps({
+          "sample": list(inspect.signature(test.sample_images).parameters)[:5],
+          "n_default": inspect.signature(test.sample_images).parameters["n_timesteps"].default,
+          "load": [p for p, v in inspect.signature(test.load_model_and_scheduler).parameters.items()
+                   if v.kind == v.POSITIONAL_OR_KEYWORD],
+          "cfg": sorted(test.config), "ldm": test.config["ldm_params"]["model_channels"]}))
+    """)
+    d = json.loads(out.strip().splitlines()[-1])
+    assert d["sample"] == ["model", "scheduler", "img_cond", "audio_cond", "n_timesteps"]
+    assert d["n_default"] == 500 and d["load"] == ["config"]
+    assert d["cfg"] == ["dataset_params", "ldm_params", "train_params"] and d["ldm"] == 64
+
+
+def test_vivit_train_entry_one_argument_call():
+    """train_huggingface_model(VIVIT) reads the module-level X_train / Y_train_p / X_test /
+    Y_test_p as the reference does (huggingface_vivit_model.py:35-41)."""
+    import os
+    from conftest import PKG
+    out = run(f"""
+        import inspect, sys
+        sys.path.insert(0, {os.path.join(PKG, "lipreading")!r})
+        import huggingface_vivit_model as h
+        ps = inspect.signature(h.train_huggingface_model).parameters
+        print(list(ps)[0], all(ps[n].default is None for n in ("X_train", "Y_train", "X_test", "Y_test")))
+        try:
+            h.train_huggingface_model(object())
+        except NameError as e:
+            print("NameError", "X_train" in str(e))
+    """)
+    assert "VIVIT True" in out and "NameError True" in out

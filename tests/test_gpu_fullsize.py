@@ -1,0 +1,227 @@
+"""Correctness at the BASELINE sizes: the flash-attention kernels at
+the sequence lengths the bench runs, and whole-model forwards at configs 2 and 4.
+
+Attention (bf16, joint, 1 head, the qkv layout of QKVAttentionLegacy, unet.py:349-366):
+  * N = 262144 / D = 64 (config 2, level 0), N = 409600 / D = 64 (config 4, level 0),
+    D = 128 at 65536 (config 2) and 102400 (config 4), D = 256 at 16384 and 25600;
+  * q / k scaled by 1.5 (peaked softmax), two keys late in the sequence amplified x5 and two
+    query rows x4: rows whose running max jumps by far more than 2^16 in the last tiles
+    drive the deferred-check forward's rare path (recompute against the true max);
+  * forward: O and the saved log-sum-exp on 256 sampled query rows (the first and last
+    tiles, the amplified rows, random rows) against a torch fp32 reference of
+    softmax(q k^T / sqrt(D)) v computed from the same bf16-rounded inputs, with the kernels'
+    one deliberate operand rounding (q, or k for dK/dV, pre-multiplied by
+    scale*log2(e) in bf16: its logit error grows with |logit|, 0.2 at a logit of 100);
+  * backward: dQ on the sampled rows, dK / dV on 256 sampled key rows (first / last tiles,
+    the amplified keys, random keys); the reference needs every row's log-sum-exp and
+    delta = rowsum(dO * O), computed exactly in fp32 by chunks of 2048 query rows.
+Tolerances (bf16 storage, bf16 P / dS operands, fp32 softmax and accumulation): rel-L2
+2e-2 (O), 4e-2 (gradients); |lse - lse_ref| <= 1e-3 + 1e-4 |lse_ref| (fp32 statistics).
+
+Whole model (UNet3D of train.py:88-97, dims=3, joint attention, audio-conditioned):
+  * config 2 (128x128x16): bf16 forward vs the same weights in fp32 parity mode, rel-L2 <=
+    3e-2 (the survey's bf16 bar; torch's own bf16 autocast gives 1.1e-2);
+  * config 4 (256x256x25): the bf16 forward is finite and agrees (rel-L2 <= 3e-2) with the
+    same forward on the plain 4-wave attention kernels (no deferred check, no pipelining,
+    KV split) -- an fp32 parity forward at this size (3951 TFLOP) does not fit a test;
+  * the 200-channel first conv at config 4 (1.6 M pixels, int64 offsets) against torch's
+    fp32 conv3d on the same bf16 inputs.
+"""
+import json
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _record(**kw):
+    """Measured errors -> $VDIFF_TEST_METRICS (JSON lines), when set (tools/gpu_check.sh)."""
+    path = os.environ.get("VDIFF_TEST_METRICS")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(kw) + "\n")
+
+
+def _fwd_with_lse(qkv_cl, C):
+    """(out [N, C] bf16, lse [N] fp32) through the C-ABI (vd_attention_fwd_ws)."""
+    from vdiff import _lib, ops
+    B, C3, N = qkv_cl.shape
+    (d, qo, ko, vo, oo), = ops._attn_desc(B, N, C, 1, C, "joint", None, _lib.VD_BF16, True)
+    out = ops.empty_cl([B, C, N], torch.bfloat16, qkv_cl.device)
+    lse = torch.empty(N, dtype=torch.float32, device=qkv_cl.device)
+    nws = _lib.lib().vd_attention_fwd_workspace_size(d)
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=qkv_cl.device)
+    es, base = 2, qkv_cl.data_ptr()
+    _lib.call("vd_attention_fwd_ws", d, base + qo * es, base + ko * es, base + vo * es,
+              out.data_ptr(), lse.data_ptr(), ws.data_ptr(), nws,
+              torch.cuda.current_stream().cuda_stream)
+    return out[0].t(), lse
+
+
+def _inputs(N, C, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    t = torch.randn((N, 3 * C), generator=g, device=dev)
+    t[:, :2 * C] *= 1.5
+    hot_k = [N - 70, N - 9]
+    hot_q = [N // 3, N - 40]
+    t[hot_k, C:2 * C] *= 5.0
+    t[hot_q, :C] *= 4.0
+    t = t.bfloat16()
+    dout = torch.randn((N, C), generator=g, device=dev).bfloat16()
+    gi = torch.Generator().manual_seed(seed + 1)
+    rnd = torch.randperm(N, generator=gi)[:256 - 68].tolist()
+    rows = sorted(set(list(range(32)) + list(range(N - 32, N)) + hot_q + hot_k + rnd))[:256]
+    return t, dout, rows, hot_k
+
+
+LN2 = math.log(2.0)
+
+
+def _prescale(u, C):
+    """The kernels' one deliberate operand rounding: q (forward, dQ) or k (dK/dV) times
+    scale * log2(e) in fp32, rounded to bf16 (RNE), so S comes out of the MFMA in log2
+    units (the reference's own bf16 path rounds q*scale and k*scale, unet.py:360-363)."""
+    c = torch.tensor(1.0 / math.sqrt(C), dtype=torch.float32) * \
+        torch.tensor(1.4426950408889634, dtype=torch.float32)
+    return (u.float() * c.to(u.device)).bfloat16().float()
+
+
+def _reference(t32, dout32, rows, keys, C, chunk=2048):
+    """fp32 torch reference, with the kernels' operand rounding, of the forward on `rows`
+    (O, natural-log lse) and of dQ[rows], dK[keys], dV[keys]."""
+    q, k, v = t32[:, :C], t32[:, C:2 * C], t32[:, 2 * C:]
+    N = q.shape[0]
+    scale = 1.0 / math.sqrt(C)
+    qs, ks = _prescale(q, C), _prescale(k, C)
+    # every row's log2-sum-exp and O (for delta), by chunks of query rows
+    lse2 = torch.empty(N, device=dev)
+    o = torch.empty(N, C, device=dev)
+    for i in range(0, N, chunk):
+        s2 = qs[i:i + chunk] @ k.t()
+        m = torch.logsumexp(s2 * LN2, dim=1) / LN2
+        lse2[i:i + chunk] = m
+        o[i:i + chunk] = torch.exp2(s2 - m[:, None]) @ v
+        del s2
+    delta = (dout32 * o).sum(1)
+    r = torch.tensor(rows, device=dev)
+    p = torch.exp2(qs[r] @ k.t() - lse2[r][:, None])
+    ds = p * (dout32[r] @ v.t() - delta[r][:, None])
+    dq = (ds @ k) * scale
+    kk = torch.tensor(keys, device=dev)
+    pc = torch.exp2(q @ ks[kk].t() - lse2[:, None])   # [N, keys], the dK/dV kernel's P
+    dsc = pc * (dout32 @ v[kk].t() - delta[:, None])
+    dk = (dsc.t() @ q) * scale
+    dv = pc.t() @ dout32
+    return o[r], lse2[r] * LN2, dq, dk, dv
+
+
+@pytest.mark.parametrize("N,C", [(262144, 64), (409600, 64), (65536, 128), (102400, 128),
+                                 (16384, 256), (25600, 256)])
+def test_attention_full_length(N, C):
+    from vdiff import ops
+    t, dout, rows, hot_k = _inputs(N, C, 1000 + C)
+    gi = torch.Generator().manual_seed(7)
+    keys = sorted(set(list(range(32)) + list(range(N - 32, N)) + hot_k
+                      + torch.randperm(N, generator=gi)[:190].tolist()))[:256]
+    qkv = t[None].transpose(1, 2)                     # logical [1, 3C, N], channels-last
+    out, lse = _fwd_with_lse(qkv, C)
+    o_ref, lse_ref, dq_ref, dk_ref, dv_ref = _reference(t.float(), dout.float(), rows, keys, C)
+    r = torch.tensor(rows, device=dev)
+    assert torch.isfinite(out.float()).all()
+    err = (lse[r] - lse_ref).abs()
+    e_o = _rel(out[r], o_ref)
+    # backward through the autograd op (the path the model runs)
+    x = qkv.detach().clone().requires_grad_(True)
+    y = ops.attention(x, heads=1)
+    assert torch.equal(y[0].t()[r], out[r])            # same kernel, same bits
+    y.backward(dout[None].transpose(1, 2))
+    g = x.grad[0].t()                                 # [N, 3C]
+    kk = torch.tensor(keys, device=dev)
+    assert torch.isfinite(g.float()).all()
+    e = dict(o=e_o, lse_max_abs=float(err.max()), dq=_rel(g[r, :C], dq_ref),
+             dk=_rel(g[kk, C:2 * C], dk_ref), dv=_rel(g[kk, 2 * C:], dv_ref))
+    _record(test="attention", N=N, C=C, **e)
+    assert e["o"] < 2e-2
+    assert bool((err <= 1e-3 + 1e-4 * lse_ref.abs()).all()), e["lse_max_abs"]
+    assert e["dq"] < 4e-2 and e["dk"] < 4e-2 and e["dv"] < 4e-2, e
+
+
+def _model(size, frames):
+    from vdiff.engine import reinit_nonzero
+    from vdiff.unet_audio import UNetAudio
+    torch.manual_seed(1234)  # the default (non-zero) layer init draws from the global RNG
+    m = UNetAudio(image_size=size, in_channels=3, model_channels=64, out_channels=3,
+                  num_res_blocks=2, attention_resolutions=(1, 2, 4), audio_feature_dim=768,
+                  projected_audio_dim=128, dims=3, use_bf16=True, audio_encoder=False)
+    reinit_nonzero(m, seed=1234)
+    return m.to(dev).eval()
+
+
+def _model_inputs(size, frames, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.rand((1, 3, frames, size, size), generator=g, device=dev) * 2 - 1
+    cond = torch.rand((1, 3, size, size), generator=g, device=dev) * 2 - 1
+    feat = torch.randn((frames, 768), generator=g, device=dev)
+    return x, cond, feat, torch.tensor([37], device=dev)
+
+
+@torch.no_grad()
+def test_config2_model_bf16_vs_fp32():
+    m = _model(128, 16)
+    x, cond, feat, t = _model_inputs(128, 16, 5)
+    y16 = m(x, cond, feat, t).float()
+    m.convert_to_fp32()
+    y32 = m(x, cond, feat, t).float()
+    assert torch.isfinite(y16).all() and torch.isfinite(y32).all()
+    assert y32.abs().max() > 0
+    e = _rel(y16, y32)
+    _record(test="config2_bf16_vs_fp32", rel_l2=e)
+    assert e < 3e-2
+
+
+@torch.no_grad()
+def test_config4_model_bf16_kernel_variants_agree():
+    from vdiff import ops
+    m = _model(256, 25)
+    x, cond, feat, t = _model_inputs(256, 25, 6)
+    y = m(x, cond, feat, t).float()
+    assert torch.isfinite(y).all() and y.abs().max() > 0
+    with ops.attention_config("base"):
+        yb = m(x, cond, feat, t).float()
+    e = _rel(y, yb)
+    _record(test="config4_default_vs_base", rel_l2=e)
+    assert e < 3e-2  # two bf16 evaluations, each ~1e-2 from fp32 (config 2)
+
+
+@torch.no_grad()
+def test_config4_first_conv():
+    """Checked on output frames at both ends and in the middle of the clip (the last pixel
+    rows sit past 2^31 bytes of im2col addressing only through int64 offsets); the
+    reference is torch's fp32 conv3d on the matching input frames."""
+    from vdiff import ops
+    g = torch.Generator(device=dev).manual_seed(8)
+    T = 25
+    x = (torch.rand((1, 200, T, 256, 256), generator=g, device=dev) * 2 - 1).bfloat16()
+    w = torch.randn((64, 195, 3, 3, 3), generator=g, device=dev) / math.sqrt(195 * 27)
+    b = torch.randn(64, generator=g, device=dev) * 0.02
+    wp = F.pad(w, [0, 0, 0, 0, 0, 0, 0, 5])       # zero-extended to the 200 padded channels
+    y = ops.conv(ops.to_cl(x), wp, b, padding=1)
+    assert list(y.shape) == [1, 64, T, 256, 256]
+    wr = wp.bfloat16().float()
+    for t0, t1 in ((0, 2), (12, 14), (T - 2, T)):
+        lo, hi = max(t0 - 1, 0), min(t1 + 1, T)
+        xs = F.pad(x[:, :, lo:hi].float(), (0, 0, 0, 0, int(t0 == 0), int(t1 == T)))
+        ref = F.conv3d(xs, wr, b, padding=(0, 1, 1))
+        e = _rel(y[:, :, t0:t1].float(), ref)
+        _record(test="config4_first_conv", frames=[t0, t1], rel_l2=e)
+        assert e < 1e-2, (t0, t1)

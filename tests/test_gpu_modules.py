@@ -286,3 +286,42 @@ def test_schedulers_module_api():
     rxp, _ = osch.ddim_step(v2.alpha_cum_prod, x0, eps, torch.tensor([499, 499]),
                             torch.tensor([int(ddim.prev_timesteps[0])] * 2))
     assert rel_l2(xp, rxp) < 1e-5
+
+
+def test_trainer_step_matches_reference_adam_step():
+    """one fp32 Trainer.step (q_sample -> UNetAudio -> MSE -> backward -> fused
+    Adam lr 1e-2) with injected eps / t against the reference train step's loss, gradients
+    and one-step parameter deltas (tests/golden/train_step_tiny3d.npz, config 1's shape)."""
+    from oracle.fixtures import adam_delta_close, train_step_inputs
+    from vdiff.engine import Clip, Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    from vdiff.unet_audio import UNetAudio
+    g = golden("train_step_tiny3d.npz")
+    m = UNetAudio(image_size=64, in_channels=3, model_channels=32, out_channels=3,
+                  num_res_blocks=1, attention_resolutions=(2,), channel_mult=(1, 2), dims=3,
+                  audio_feature_dim=64, projected_audio_dim=16, im_cond_output_ch=16,
+                  dropout=0.0, audio_encoder=False)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    P = init_params({k: v for k, v in shapes.items() if not k.startswith(("audio_", "cond_"))},
+                    1234)
+    P.update(init_params(audio_param_shapes(64, 16, im_cond_output_ch=16), 77))
+    m.load_state_dict(P)
+    m = m.to(dev)
+    before = {k: v.detach().clone() for k, v in m.named_parameters()}
+    x0, cond, feat, eps = (u.to(dev) for u in train_step_inputs())
+    tr = Trainer(m, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2)
+    grads = {}
+    hooks = [p.register_post_accumulate_grad_hook(
+        lambda p, n=n: grads.__setitem__(n, p.grad.detach().clone()))
+        for n, p in m.named_parameters()]
+    loss = tr.step(Clip(x0, cond, feat, eps, g["t"].to(dev)))
+    for h in hooks:
+        h.remove()
+    assert abs(float(loss) - float(g["loss"])) < 1e-5 * float(g["loss"])
+    named = dict(m.named_parameters())
+    keys = [k[len("delta_"):] for k in g if k.startswith("delta_")]
+    assert len(keys) == 9
+    for k in keys:
+        assert rel_l2(grads[k], g["grad_" + k]) < 1e-4, k
+        d = named[k].detach() - before[k]
+        assert adam_delta_close(d, g["delta_" + k], g["grad_" + k]) < 1e-6, k

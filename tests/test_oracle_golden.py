@@ -174,3 +174,22 @@ def test_full2d_unet_and_audio_conditioning():
                                     128)
     y = unet_forward(P, plan, feats, ga["t"])
     assert rel_l2(y, ga["y"]) < 1e-5
+
+
+def test_one_adam_train_step():
+    """the oracle's train step (q_sample -> conditioning -> UNet -> MSE -> bwd ->
+    Adam(lr 1e-2)) against the reference's (train.py:122-134) at config 1's shape."""
+    from oracle.fixtures import adam_delta_close, train_step_inputs
+    from oracle.train import train_step
+    g = golden("train_step_tiny3d.npz")
+    plan = build_plan(**TINY3D)
+    P = init_params(param_shapes(plan), 1234)
+    P.update(init_params(audio_param_shapes(64, 16, im_cond_output_ch=16), 77))
+    x0, cond, feat, eps = train_step_inputs()
+    loss, grads, deltas = train_step(P, plan, x0, cond, feat, eps, g["t"], 16)
+    close(loss, g["loss"], atol=1e-6, rtol=1e-5)
+    names = [k[len("delta_"):] for k in g if k.startswith("delta_")]
+    assert len(names) == 9
+    for k in names:
+        assert rel_l2(grads[k], g["grad_" + k]) < 1e-4, k
+        assert adam_delta_close(deltas[k], g["delta_" + k], g["grad_" + k]) < 1e-6, k
