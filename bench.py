@@ -70,6 +70,9 @@ def parse():
                     help="no HIP-graph capture of the ViViT step")
     ap.add_argument("--vivit-graph-ddp", action="store_true",
                     help="N > 1: graph-captured ViViT step around one all-reduce")
+    ap.add_argument("--xattn-steps", type=int, default=3,
+                    help="timed train steps with audio cross-attention (build extension, "
+                         "auxiliary leg); 0 skips it")
     ap.add_argument("--c4-steps", type=int, default=3,
                     help="timed DDIM steps at BASELINE config 4 (256x256x25); 0 skips the leg")
     return ap.parse_args()
@@ -80,7 +83,7 @@ def log(*a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def build_model(args, device):
+def build_model(args, device, audio_attention=False):
     from vdiff.engine import reinit_nonzero
     from vdiff.unet_audio import UNetAudio
     import warnings
@@ -90,7 +93,7 @@ def build_model(args, device):
                           num_res_blocks=2, attention_resolutions=(1, 2, 4),
                           audio_feature_dim=768, projected_audio_dim=128, dims=3,
                           use_bf16=args.dtype == "bf16", attention_mode=args.mode,
-                          audio_encoder_pretrained=False)
+                          audio_encoder_pretrained=False, audio_attention=audio_attention)
     reinit_nonzero(model, seed=1234)
     return model.to(device)
 
@@ -324,6 +327,41 @@ def vivit_leg(args, rank, world, device):
     return out
 
 
+def xattn_leg(args, rank, world, device, base_ms):
+    """Auxiliary: the same train step with the audio cross-attention branches on
+    (audio_attention=True, build extension): every attention block also attends from the
+    video tokens to the 12 wav2vec2 tokens of each frame's audio window."""
+    from vdiff.ddp import broadcast_parameters
+    from vdiff.engine import Trainer, synthetic_clip
+    from vdiff.flops import unet_forward_work
+    from vdiff.schedulers import LinearNoiseScheduler
+    torch.manual_seed(1234 + rank)
+    model = build_model(args, device, audio_attention=True)
+    broadcast_parameters(model)
+    work = unet_forward_work(model, (args.clips_per_gpu, 195, args.frames, args.size, args.size))
+    tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2)
+    clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
+    for _ in range(2):
+        tr.step(clip)
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(args.xattn_steps):
+        loss = tr.step(clip)
+    barrier_sync(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, device)
+    ms = el / args.xattn_steps * 1e3
+    out = {"metric": "train-step frames/sec with audio cross-attention (build extension)",
+           "value": round(world * args.clips_per_gpu * args.frames * args.xattn_steps / el, 4),
+           "unit": "frames/s", "ms_per_step": round(ms, 2),
+           "overhead_ms_vs_concat_only": round(ms - base_ms, 2) if base_ms else None,
+           "fwd_tflop_per_clip": round(work.total / 1e12, 3), "audio_tokens_per_frame": 12,
+           "loss": round(float(loss), 4)}
+    log(f"xattn: {ms:.1f} ms/step")
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     from vdiff import ops
@@ -458,6 +496,14 @@ def main():
             torch.cuda.empty_cache()
         if "value" not in result:
             result.update(value=ddim["value"], unit="steps/s", ms_per_step=ddim["ms_per_step"])
+
+    if args.only in ("train", "all") and args.xattn_steps > 0:
+        try:  # an auxiliary leg: never let it take the headline numbers down
+            result["audio_xattn"] = xattn_leg(args, rank, world, device,
+                                              result.get("ms_per_step"))
+        except Exception as e:
+            log(f"xattn leg failed: {type(e).__name__}: {e}")
+            result["audio_xattn"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
 
     if args.only in ("vivit", "all") and args.vivit_steps > 0:
         try:  # an auxiliary leg: never let it take the headline numbers down

@@ -256,6 +256,35 @@ int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k,
                           const void* v, const void* dout, const float* lse,
                           void* dk, void* dv, void* workspace, void* stream);
 
+/* ---- audio cross-attention (north_star build extension; no reference counterpart: the
+ * reference conditions on audio by channel concatenation only, unet_audio.py:52-61).
+ * Video tokens attend to audio tokens: softmax(scale * q k^T) v with q / o addressed by
+ * `q` (as vd_attn_desc: nseq, seq_len = N_q, head_dim, groups, q and o strides, scale,
+ * dtype) and k / v rows by the kv_* fields: sequence i's K/V rows start at
+ * (i / q.groups) * kv_batch_stride + (i % q.groups) * kv_group_stride, kv_token_stride
+ * apart, kv_len of them (N_kv may differ from N_q).  lse fp32 [nseq][N_q] as above.  The
+ * backward has the self-attention contract (dq in the q strides, dk / dv in the kv
+ * strides, overwritten); where the K/V grid leaves CUs idle (bf16, few audio tokens) the
+ * queries are split and the fp32 dK / dV partials summed by a second kernel, inside the
+ * workspace. */
+typedef struct vd_xattn_desc {
+  vd_attn_desc q;
+  int kv_len;
+  int64_t kv_batch_stride, kv_group_stride, kv_token_stride;
+} vd_xattn_desc;
+
+size_t vd_cross_attention_fwd_workspace_size(const vd_xattn_desc* x);
+int vd_cross_attention_fwd(const vd_xattn_desc* x, const void* q, const void* k,
+                           const void* v, void* o, float* lse, void* workspace,
+                           size_t workspace_bytes, void* stream);
+size_t vd_cross_attention_bwd_workspace_size(const vd_xattn_desc* x);
+int vd_cross_attention_bwd_dq(const vd_xattn_desc* x, const void* q, const void* k,
+                              const void* v, const void* o, const void* dout,
+                              const float* lse, void* dq, void* workspace, void* stream);
+int vd_cross_attention_bwd_dkdv(const vd_xattn_desc* x, const void* q, const void* k,
+                                const void* v, const void* dout, const float* lse,
+                                void* dk, void* dv, void* workspace, void* stream);
+
 /* ---- ViViT lipreading encoder ops (lipreading/huggingface_vivit_model.py:18-33
  * over transformers' VivitModel: VivitLayer.layernorm_before/_after, final layernorm, VivitMLP
  * with hidden_act "gelu_fast").

@@ -356,6 +356,15 @@ struct SeqAddr {
   }
 };
 
+// The K/V rows of sequence i: self-attention uses the query's own addressing; cross-
+// attention (vd_cross_attention_*) has a K/V buffer of its own, with its own length and
+// strides (e.g. the audio tokens of a frame).
+struct KvAddr {
+  SeqAddr a;
+  int64_t ts;  // token stride of the K/V rows
+  int n;       // K/V rows per sequence
+};
+
 
 // ------------------------------------------------------------------ tile pipelines
 // bf16: LDS ring of NST stages filled by buffer_load ... lds (LDS-DMA, no register
@@ -664,7 +673,7 @@ template <typename T, int D, int NB, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale,
-    FwdSplit split) {
+    FwdSplit split, KvAddr kv) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int seq = blockIdx.y;
@@ -672,8 +681,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
   const int64_t base = qa(seq);
   // this workgroup's keys: [kofs, kofs + nk)
   const int kofs = blockIdx.z * split.tps * kTile;
-  const int nk = split.part ? min(n - kofs, split.tps * kTile) : n;
-  const int64_t kbase = base + (int64_t)kofs * ts;
+  const int nk = split.part ? min(kv.n - kofs, split.tps * kTile) : kv.n;
+  const int64_t kbase = kv.a(seq) + (int64_t)kofs * kv.ts;
 
   RowFrag<T, D> qf[NB];
 #pragma unroll
@@ -696,7 +705,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_kernel(
     for (int r = 0; r < 16; ++r) negm[j][r] = INFINITY;
   }
 
-  tile_loop<T, D, false, NW>(smem, k + kbase, v + kbase, ts, ts, nullptr, nullptr, nk, tid,
+  tile_loop<T, D, false, NW>(smem, k + kbase, v + kbase, kv.ts, kv.ts, nullptr, nullptr, nk, tid,
                          [&](int t, const T* Kt, const T* Vt, const float*) {
     const int key0 = t * kTile;
     const bool tail = key0 + kTile > nk;  // only the last tile masks keys (wave-uniform)
@@ -919,15 +928,15 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
     const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
     T* __restrict__ dq, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale,
-    FwdSplit split) {
+    FwdSplit split, KvAddr kv) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int seq = blockIdx.y;
   const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
   const int kofs = blockIdx.z * split.tps * kTile;
-  const int nk = split.part ? min(n - kofs, split.tps * kTile) : n;
-  const int64_t kbase = base + (int64_t)kofs * ts;
+  const int nk = split.part ? min(kv.n - kofs, split.tps * kTile) : kv.n;
+  const int64_t kbase = kv.a(seq) + (int64_t)kofs * kv.ts;
 
   RowFrag<T, D> qf[NB], of[NB];
   f32x16 il[NB], id[NB];
@@ -951,7 +960,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_kernel(
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
 
-  tile_loop<T, D, false, NW>(smem, k + kbase, v + kbase, ts, ts, nullptr, nullptr, nk, tid,
+  tile_loop<T, D, false, NW>(smem, k + kbase, v + kbase, kv.ts, kv.ts, nullptr, nullptr, nk, tid,
                          [&](int, const T* Kt, const T* Vt, const float*) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1023,20 +1032,28 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
     const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
     T* __restrict__ dk, T* __restrict__ dv, int n, SeqAddr qa, int64_t ts, SeqAddr oa,
-    int64_t ots, float scale) {
+    int64_t ots, float scale, KvAddr kv, FwdSplit qsplit) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int seq = blockIdx.y;
-  const int d0 = blockIdx.z * DO;
+  constexpr int NZ = D / DO;
+  const int d0 = (blockIdx.z % NZ) * DO;
+  // query split (grids too small for the chip, e.g. cross-attention onto a few audio
+  // tokens): z takes the query tiles [qz * tps, (qz + 1) * tps) and writes fp32 partial
+  // dK / dV; attn_dkdv_sum_kernel adds the splits
+  const int qz = blockIdx.z / NZ;
+  const int qofs = qz * qsplit.tps * kTile;
+  const int nq = qsplit.part ? min(n - qofs, qsplit.tps * kTile) : n;
   const int k0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
-  const int64_t base = qa(seq), obase = oa(seq);
+  const int64_t base = qa(seq) + (int64_t)qofs * ts, obase = oa(seq) + (int64_t)qofs * ots;
+  const int64_t kb = kv.a(seq);
 
   RowFrag<T, D> kf[NB], vf[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    kf[j].load(k + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+    kf[j].load(k + kb, kv.ts, k0 + 32 * j + (lane & 31), kv.n, lane);
     kf[j].scale(scale * kLog2e);
-    vf[j].load(v + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+    vf[j].load(v + kb, kv.ts, k0 + 32 * j + (lane & 31), kv.n, lane);
   }
   f32x16 adv[DO / 32][NB], adk[DO / 32][NB];
 #pragma unroll
@@ -1046,8 +1063,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
 
   // query rows past n have zero Q / dO rows and zero row constants, so they add nothing
   // to dV (dO = 0) or dK (dS = p * (0 - 0)): no mask needed.
-  tile_loop<T, D, true, NW>(smem, q + base, dout + obase, ts, ots, nlse2 + (int64_t)seq * n,
-                        ndelta + (int64_t)seq * n, n, tid,
+  tile_loop<T, D, true, NW>(smem, q + base, dout + obase, ts, ots,
+                        nlse2 + (int64_t)seq * n + qofs, ndelta + (int64_t)seq * n + qofs, nq, tid,
                         [&](int, const T* Qt, const T* Ot, const float* L) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1096,8 +1113,39 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
       ok[i] = adk[i][j];
       ov[i] = adv[i][j];
     }
-    store_transposed<T, DO / 32>(dk + base, ts, mykey, n, d0, ok, scale, lane);
-    store_transposed<T, DO / 32>(dv + base, ts, mykey, n, d0, ov, 1.f, lane);
+    if (qsplit.part) {
+      float* pb = qsplit.part + ((int64_t)qz * gridDim.y + seq) * kv.n * (2 * D);
+      store_transposed<float, DO / 32>(pb, 2 * D, mykey, kv.n, d0, ok, scale, lane);
+      store_transposed<float, DO / 32>(pb + D, 2 * D, mykey, kv.n, d0, ov, 1.f, lane);
+    } else {
+      store_transposed<T, DO / 32>(dk + kb, kv.ts, mykey, kv.n, d0, ok, scale, lane);
+      store_transposed<T, DO / 32>(dv + kb, kv.ts, mykey, kv.n, d0, ov, 1.f, lane);
+    }
+  }
+}
+
+// dK | dV = sum over the query splits of the fp32 partials [split][nseq][nkv][dK D | dV D]
+// (one thread per 8 columns)
+template <typename T, int D>
+__global__ void attn_dkdv_sum_kernel(const float* __restrict__ part, int splits, int nseq,
+                                     int nkv, T* __restrict__ dk, T* __restrict__ dv, SeqAddr ka,
+                                     int64_t kts) {
+  constexpr int CPR = 2 * D / 8;
+  const int64_t rows = (int64_t)nseq * nkv;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * CPR;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / CPR;
+    const int c8 = (int)(i % CPR) * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int z = 0; z < splits; ++z) {
+      float v8[8];
+      load8(part + ((int64_t)z * rows + row) * (2 * D) + c8, v8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v8[e];
+    }
+    const int seq = (int)(row / nkv), tok = (int)(row % nkv);
+    T* dst = (c8 < D ? dk + c8 : dv + (c8 - D)) + ka(seq) + (int64_t)tok * kts;
+    store8(dst, acc);
   }
 }
 
@@ -1645,36 +1693,76 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
 
 // KV splits for a query grid of `wgs` workgroups: enough to give every CU one (>= 256),
 // at most 4, at least 4 key tiles each; 1 = no split.  bf16 only.
-int kv_splits(const vd_attn_desc* d, int64_t wgs) {
+int kv_splits(const vd_attn_desc* d, int64_t wgs, int nkv) {
   if (d->dtype != VD_BF16 || wgs >= 256) return 1;
   int s = (int)((256 + wgs - 1) / wgs);
   if (s > 4) s = 4;
+  const int64_t tiles = vd_cdiv(nkv, kTile);
+  while (s > 1 && tiles / s < 4) --s;
+  return s;
+}
+int split_tps(int len, int s) { return (int)vd_cdiv(vd_cdiv(len, kTile), s); }
+
+KvAddr self_kv(const vd_attn_desc* d) {
+  return KvAddr{SeqAddr{d->batch_stride, d->group_stride, d->groups}, d->token_stride,
+                d->seq_len};
+}
+
+// dK/dV output-column slice of the 4-wave generic kernel (register budget at D = 256)
+template <int D, int NW> constexpr int dkdv_do() { return D > 128 ? 128 : (D == 128 && NW == 8 ? 64 : D); }
+
+// Query splits of the 4-wave dK/dV kernel when its key grid leaves CUs idle (bf16):
+// at most 16, at least 4 query tiles each; 1 = no split.
+template <int D>
+int q_splits(const vd_attn_desc* d, int nkv) {
+  if (d->dtype != VD_BF16) return 1;
+  const int64_t wgs = vd_cdiv(nkv, 128) * d->nseq * (D / dkdv_do<D, 4>());
+  if (wgs >= 256) return 1;
+  int s = (int)((256 + wgs - 1) / wgs);
+  if (s > 16) s = 16;
   const int64_t tiles = vd_cdiv(d->seq_len, kTile);
   while (s > 1 && tiles / s < 4) --s;
   return s;
 }
-int split_tps(const vd_attn_desc* d, int s) {
-  return (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), s);
+
+// Backward workspace: [ndelta rows][nlse2 rows][64 floats][dQ KV-split partials]
+// [dK/dV query-split partials]; rows = nseq * seq_len (queries).
+struct BwdWs {
+  int sdq, sq;       // KV splits of the dQ pass, query splits of the dK/dV pass
+  size_t dq_off, kv_off, bytes;  // float offsets of the partials; total bytes
+};
+template <int D>
+BwdWs bwd_ws(const vd_attn_desc* d, int nkv, bool cross) {
+  BwdWs w{1, 1, 0, 0, 0};
+  const size_t rows = (size_t)d->nseq * d->seq_len;
+  if (d->dtype == VD_BF16 && (cross || pick_cfg(D, true, 1) == kBase))
+    w.sdq = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv);
+  if (cross || (d->dtype == VD_BF16 && pick_cfg(D, true, 2) == kBase)) w.sq = q_splits<D>(d, nkv);
+  w.dq_off = 2 * rows + 64;
+  w.kv_off = w.dq_off + (w.sdq > 1 ? (size_t)w.sdq * rows * D : 0);
+  const size_t kvp = w.sq > 1 ? (size_t)w.sq * d->nseq * nkv * 2 * D : 0;
+  w.bytes = (w.kv_off + kvp) * sizeof(float);
+  return w;
 }
 
 template <typename T, int D, int NB, int NW>
-int fwd_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
-               float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
+int fwd_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k, const void* v,
+               void* o, float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
   const size_t lds = tile_loop_lds<T, D, false>();
   auto kern = attn_fwd_kernel<T, D, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int64_t qwg = vd_cdiv(d->seq_len, 32 * NB * NW);
-  int s = kv_splits(d, qwg * d->nseq);
+  int s = kv_splits(d, qwg * d->nseq, kv.n);
   const size_t need = (size_t)s * d->nseq * d->seq_len * (D + 2) * sizeof(float);
   if (s > 1 && (!ws || ws_bytes < need)) s = 1;
-  FwdSplit split{s > 1 ? (float*)ws : nullptr, split_tps(d, s)};
-  if (s > 1) s = (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), split.tps);
+  FwdSplit split{s > 1 ? (float*)ws : nullptr, split_tps(kv.n, s)};
+  if (s > 1) s = (int)vd_cdiv(vd_cdiv(kv.n, kTile), split.tps);
   dim3 grid((unsigned)qwg, (unsigned)d->nseq, (unsigned)s);
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
                                    d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
-                                   d->token_stride, oa, d->o_token_stride, d->scale, split);
+                                   d->token_stride, oa, d->o_token_stride, d->scale, split, kv);
   if (s > 1) {
     const int rc = vd::check_launch("attn_fwd");
     if (rc) return rc;
@@ -1689,10 +1777,10 @@ int fwd_launch(const vd_attn_desc* d, const void* q, const void* k, const void* 
 
 // bytes of the KV-split forward workspace of this shape (0: no split is used)
 template <int D>
-size_t fwd_ws_bytes(const vd_attn_desc* d) {
+size_t fwd_ws_bytes(const vd_attn_desc* d, int nkv, bool cross) {
   if (d->dtype != VD_BF16) return 0;
-  if (pick_cfg(D, true, 0) != kBase) return 0;  // only the 4-wave, 32-row shape splits
-  const int s = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq);
+  if (!cross && pick_cfg(D, true, 0) != kBase) return 0;  // only the 4-wave shape splits
+  const int s = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv);
   return s > 1 ? (size_t)s * d->nseq * d->seq_len * (D + 2) * sizeof(float) : 0;
 }
 
@@ -1729,14 +1817,15 @@ int fwd_defer_launch(const vd_attn_desc* d, const void* q, const void* k, const 
 }
 
 template <typename T, int D>
-int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
-             float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
-  if constexpr (kDMA<T>) {
+int fwd_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
+             const void* v, void* o, float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
+  // cross-attention runs on the generic 4-wave kernel (its K/V sequences are short)
+  if constexpr (kDMA<T>) if (!cross) {
     const AttnCfg c = pick_cfg(D, true, 0);
     if constexpr (D != 256)
-      if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, q, k, v, o, lse, nullptr, 0, st);
+      if (c == kNB2) return fwd_launch<T, D, 2, 4>(d, kv, q, k, v, o, lse, nullptr, 0, st);
     if constexpr (D == 64 || D == 128)
-      if (c == kW8) return fwd_launch<T, D, 1, 8>(d, q, k, v, o, lse, nullptr, 0, st);
+      if (c == kW8) return fwd_launch<T, D, 1, 8>(d, kv, q, k, v, o, lse, nullptr, 0, st);
     if constexpr (D == 64) {
       if (c == kP8) return fwd_pipe_launch<T, D, 8>(d, q, k, v, o, lse, st);
       if (c == kD8) return fwd_defer_launch<T, D, 8, true>(d, q, k, v, o, lse, st);
@@ -1748,13 +1837,13 @@ int fwd_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
     if constexpr (D <= 128)
       if (c == kP4) return fwd_pipe_launch<T, D, 4>(d, q, k, v, o, lse, st);
   }
-  return fwd_launch<T, D, 1, 4>(d, q, k, v, o, lse, ws, ws_bytes, st);
+  return fwd_launch<T, D, 1, 4>(d, kv, q, k, v, o, lse, ws, ws_bytes, st);
 }
 
 template <typename T, int D, int NB, int NW>
-int dq_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+int dq_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k, const void* v,
               const void* dout, const float* nlse2, const float* ndelta, void* dq,
-              hipStream_t st, float* part = nullptr) {
+              hipStream_t st, float* part = nullptr, int sdq = 1) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const size_t lds = tile_loop_lds<T, D, false>();
@@ -1762,13 +1851,13 @@ int dq_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int64_t qwg = vd_cdiv(d->seq_len, 32 * NB * NW);
-  int s = part ? kv_splits(d, qwg * d->nseq) : 1;
-  FwdSplit split{s > 1 ? part : nullptr, split_tps(d, s)};
-  if (s > 1) s = (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), split.tps);
+  int s = part ? sdq : 1;
+  FwdSplit split{s > 1 ? part : nullptr, split_tps(kv.n, s)};
+  if (s > 1) s = (int)vd_cdiv(vd_cdiv(kv.n, kTile), split.tps);
   dim3 grid((unsigned)qwg, (unsigned)d->nseq, (unsigned)s);
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
                                    ndelta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
-                                   d->o_token_stride, d->scale, split);
+                                   d->o_token_stride, d->scale, split, kv);
   if (s > 1) {
     const int rc = vd::check_launch("attn_bwd_dq");
     if (rc) return rc;
@@ -1799,8 +1888,9 @@ int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
 }
 
 template <typename T, int D>
-int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v, const void* o,
-                const void* dout, const float* lse, void* dq, void* ws, hipStream_t st) {
+int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
+                const void* v, const void* o, const void* dout, const float* lse, void* dq,
+                void* ws, hipStream_t st) {
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const int64_t rows = (int64_t)d->nseq * d->seq_len;
   float* ndelta = reinterpret_cast<float*>(ws);  // workspace: [ndelta rows][nlse2 rows]
@@ -1811,12 +1901,12 @@ int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void*
                                               d->nseq, d->seq_len, oa, d->o_token_stride);
   int rc = vd::check_launch("attn_delta");
   if (rc) return rc;
-  if constexpr (kDMA<T>) {
+  if constexpr (kDMA<T>) if (!cross) {
     const AttnCfg c = pick_cfg(D, true, 1);
     if constexpr (D != 256)
-      if (c == kNB2) return dq_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+      if (c == kNB2) return dq_launch<T, D, 2, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64 || D == 128)
-      if (c == kW8) return dq_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+      if (c == kW8) return dq_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kP8) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D <= 128)
@@ -1824,27 +1914,40 @@ int bwd_dq_impl(const vd_attn_desc* d, const void* q, const void* k, const void*
   }
   // the 4-wave, 32-row shape splits the keys when its grid leaves CUs idle (bf16, D = 256):
   // fp32 partials after the row constants in the workspace (vd_attention_bwd_workspace_size)
-  return dq_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st,
-                               kDMA<T> ? nlse2 + rows + 64 : nullptr);
+  const BwdWs w = bwd_ws<D>(d, kv.n, cross);
+  return dq_launch<T, D, 1, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st,
+                               reinterpret_cast<float*>(ws) + w.dq_off, w.sdq);
 }
 
 template <typename T, int D, int NB, int NW>
-int dkdv_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+int dkdv_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k, const void* v,
                 const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
-                hipStream_t st) {
+                hipStream_t st, float* part = nullptr, int sq = 1) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   // output-column slice per workgroup (grid.z = D / DO): register budget at D = 256, and at
   // D = 128 with 8 waves (two per SIMD: 256 registers each)
-  constexpr int DO = D > 128 ? 128 : (D == 128 && NW == 8 ? 64 : D);
+  constexpr int DO = dkdv_do<D, NW>();
   const size_t lds = tile_loop_lds<T, D, true>();
   auto kern = attn_bwd_dkdv_kernel<T, D, DO, NB, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq, D / DO);
+  if (!part) sq = 1;
+  FwdSplit qsplit{sq > 1 ? part : nullptr, split_tps(d->seq_len, sq)};
+  if (sq > 1) sq = (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), qsplit.tps);
+  dim3 grid((unsigned)vd_cdiv(kv.n, 32 * NB * NW), (unsigned)d->nseq, (D / DO) * sq);
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
                                    ndelta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
-                                   d->o_token_stride, d->scale);
+                                   d->o_token_stride, d->scale, kv, qsplit);
+  if (sq > 1) {
+    const int rc = vd::check_launch("attn_bwd_dkdv");
+    if (rc) return rc;
+    const int64_t work = (int64_t)d->nseq * kv.n * (2 * D / 8);
+    int g = (int)vd_cdiv(work, 256);
+    if (g > 4096) g = 4096;
+    attn_dkdv_sum_kernel<T, D><<<g, 256, 0, st>>>(qsplit.part, sq, d->nseq, kv.n, (T*)dk,
+                                                  (T*)dv, kv.a, kv.ts);
+  }
   return vd::check_launch("attn_bwd_dkdv");
 }
 
@@ -1866,25 +1969,27 @@ int dkdv_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const 
 }
 
 template <typename T, int D>
-int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                  const void* dout, const float* lse, void* dk, void* dv, void* ws,
-                  hipStream_t st) {
+int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
+                  const void* v, const void* dout, const float* lse, void* dk, void* dv,
+                  void* ws, hipStream_t st) {
   (void)lse;  // read through the workspace copy written by the dQ pass
   const float* ndelta = reinterpret_cast<const float*>(ws);
   const float* nlse2 = ndelta + (int64_t)d->nseq * d->seq_len;
-  if constexpr (kDMA<T>) {
+  if constexpr (kDMA<T>) if (!cross) {
     // (NB = 2 above D = 64 needs > 512 registers; hipcc 7.2 also crashes on it)
     const AttnCfg c = pick_cfg(D, true, 2);
     if constexpr (D <= 64)
-      if (c == kNB2) return dkdv_launch<T, D, 2, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+      if (c == kNB2) return dkdv_launch<T, D, 2, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64 || D == 128)
-      if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+      if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kP8) return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D <= 128)
       if (c == kP4) return dkdv_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
   }
-  return dkdv_launch<T, D, 1, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+  const BwdWs w = bwd_ws<D>(d, kv.n, cross);
+  return dkdv_launch<T, D, 1, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st,
+                                 reinterpret_cast<float*>(ws) + w.kv_off, w.sq);
 }
 
 #define VD_DISPATCH_HEAD(D_, FN, ...)                        \
@@ -1895,6 +2000,67 @@ int bwd_dkdv_impl(const vd_attn_desc* d, const void* q, const void* k, const voi
     case 256: return FN<T, 256>(__VA_ARGS__);                \
     default: return vd::fail(VD_EUNSUPPORTED, "head_dim");   \
   }
+
+int check_xattn(const vd_xattn_desc* x) {
+  VD_REQUIRE(x, "null descriptor");
+  int rc = check_attn(&x->q);
+  if (rc) return rc;
+  VD_REQUIRE(x->kv_len > 0 && x->kv_token_stride > 0, "bad cross-attention K/V shape");
+  if (x->q.dtype == VD_BF16)
+    VD_REQUIRE(((int64_t)x->kv_len * x->kv_token_stride + x->q.head_dim) * 2 < 0x7fffffffLL,
+               "K/V sequence spans >= 2 GiB");
+  return VD_OK;
+}
+
+KvAddr cross_kv(const vd_xattn_desc* x) {
+  return KvAddr{SeqAddr{x->kv_batch_stride, x->kv_group_stride, x->q.groups},
+                x->kv_token_stride, x->kv_len};
+}
+
+#define VD_DISPATCH_DT(d, FN, ...)                                       \
+  do {                                                                   \
+    if ((d)->dtype == VD_BF16) {                                         \
+      using T = bf16_t;                                                  \
+      VD_DISPATCH_HEAD((d)->head_dim, FN, __VA_ARGS__);                  \
+    } else if ((d)->dtype == VD_F32) {                                   \
+      using T = float;                                                   \
+      VD_DISPATCH_HEAD((d)->head_dim, FN, __VA_ARGS__);                  \
+    }                                                                    \
+    return vd::fail(VD_EUNSUPPORTED, "dtype %d", (d)->dtype);            \
+  } while (0)
+
+int fwd_any(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
+            const void* v, void* o, float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
+  VD_DISPATCH_DT(d, fwd_impl, d, kv, cross, q, k, v, o, lse, ws, ws_bytes, st);
+}
+int dq_any(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
+           const void* v, const void* o, const void* dout, const float* lse, void* dq, void* ws,
+           hipStream_t st) {
+  VD_DISPATCH_DT(d, bwd_dq_impl, d, kv, cross, q, k, v, o, dout, lse, dq, ws, st);
+}
+int dkdv_any(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
+             const void* v, const void* dout, const float* lse, void* dk, void* dv, void* ws,
+             hipStream_t st) {
+  VD_DISPATCH_DT(d, bwd_dkdv_impl, d, kv, cross, q, k, v, dout, lse, dk, dv, ws, st);
+}
+size_t fwd_ws_any(const vd_attn_desc* d, int nkv, bool cross) {
+  switch (d->head_dim) {
+    case 32: return fwd_ws_bytes<32>(d, nkv, cross);
+    case 64: return fwd_ws_bytes<64>(d, nkv, cross);
+    case 128: return fwd_ws_bytes<128>(d, nkv, cross);
+    case 256: return fwd_ws_bytes<256>(d, nkv, cross);
+    default: return 0;
+  }
+}
+size_t bwd_ws_any(const vd_attn_desc* d, int nkv, bool cross) {
+  switch (d->head_dim) {
+    case 32: return bwd_ws<32>(d, nkv, cross).bytes;
+    case 64: return bwd_ws<64>(d, nkv, cross).bytes;
+    case 128: return bwd_ws<128>(d, nkv, cross).bytes;
+    case 256: return bwd_ws<256>(d, nkv, cross).bytes;
+    default: return 0;
+  }
+}
 
 }  // namespace
 
@@ -1916,15 +2082,8 @@ int vd_attention_fwd_ws(const vd_attn_desc* d, const void* q, const void* k, con
   int rc = check_attn(d);
   if (rc) return rc;
   VD_REQUIRE(q && k && v && o && lse, "null tensor");
-  hipStream_t st = VD_STREAM(stream);
-  if (d->dtype == VD_BF16) {
-    using T = bf16_t;
-    VD_DISPATCH_HEAD(d->head_dim, fwd_impl, d, q, k, v, o, lse, workspace, workspace_bytes, st);
-  } else if (d->dtype == VD_F32) {
-    using T = float;
-    VD_DISPATCH_HEAD(d->head_dim, fwd_impl, d, q, k, v, o, lse, workspace, workspace_bytes, st);
-  }
-  return vd::fail(VD_EUNSUPPORTED, "dtype %d", d->dtype);
+  return fwd_any(d, self_kv(d), false, q, k, v, o, lse, workspace, workspace_bytes,
+                 VD_STREAM(stream));
 }
 
 int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
@@ -1934,13 +2093,7 @@ int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const 
 
 size_t vd_attention_fwd_workspace_size(const vd_attn_desc* d) {
   if (!d || d->nseq <= 0 || d->seq_len <= 0) return 0;
-  switch (d->head_dim) {
-    case 32: return fwd_ws_bytes<32>(d);
-    case 64: return fwd_ws_bytes<64>(d);
-    case 128: return fwd_ws_bytes<128>(d);
-    case 256: return fwd_ws_bytes<256>(d);
-    default: return 0;
-  }
+  return fwd_ws_any(d, d->seq_len, false);
 }
 
 int vd_attention_set_config(int cfg) {
@@ -1953,14 +2106,7 @@ int vd_attention_set_config(int cfg) {
 
 size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d) {
   if (!d || d->nseq <= 0 || d->seq_len <= 0) return 0;
-  const size_t rows = (size_t)d->nseq * d->seq_len;
-  size_t bytes = 2 * rows * sizeof(float) + 256;  // ndelta, nlse2
-  // KV-split dQ partials (bf16, the 4-wave dQ shape when its grid leaves CUs idle)
-  if (d->dtype == VD_BF16 && pick_cfg(d->head_dim, true, 1) == kBase) {
-    const int s = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq);
-    if (s > 1) bytes += 64 * sizeof(float) + (size_t)s * rows * d->head_dim * sizeof(float);
-  }
-  return bytes;
+  return bwd_ws_any(d, d->seq_len, false);
 }
 
 int vd_attention_bwd_dq(const vd_attn_desc* d, const void* q, const void* k, const void* v,
@@ -1969,15 +2115,7 @@ int vd_attention_bwd_dq(const vd_attn_desc* d, const void* q, const void* k, con
   int rc = check_attn(d);
   if (rc) return rc;
   VD_REQUIRE(q && k && v && o && dout && lse && dq && workspace, "null tensor");
-  hipStream_t st = VD_STREAM(stream);
-  if (d->dtype == VD_BF16) {
-    using T = bf16_t;
-    VD_DISPATCH_HEAD(d->head_dim, bwd_dq_impl, d, q, k, v, o, dout, lse, dq, workspace, st);
-  } else if (d->dtype == VD_F32) {
-    using T = float;
-    VD_DISPATCH_HEAD(d->head_dim, bwd_dq_impl, d, q, k, v, o, dout, lse, dq, workspace, st);
-  }
-  return vd::fail(VD_EUNSUPPORTED, "dtype %d", d->dtype);
+  return dq_any(d, self_kv(d), false, q, k, v, o, dout, lse, dq, workspace, VD_STREAM(stream));
 }
 
 int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k, const void* v,
@@ -1986,15 +2124,8 @@ int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k, c
   int rc = check_attn(d);
   if (rc) return rc;
   VD_REQUIRE(q && k && v && dout && lse && dk && dv && workspace, "null tensor");
-  hipStream_t st = VD_STREAM(stream);
-  if (d->dtype == VD_BF16) {
-    using T = bf16_t;
-    VD_DISPATCH_HEAD(d->head_dim, bwd_dkdv_impl, d, q, k, v, dout, lse, dk, dv, workspace, st);
-  } else if (d->dtype == VD_F32) {
-    using T = float;
-    VD_DISPATCH_HEAD(d->head_dim, bwd_dkdv_impl, d, q, k, v, dout, lse, dk, dv, workspace, st);
-  }
-  return vd::fail(VD_EUNSUPPORTED, "dtype %d", d->dtype);
+  return dkdv_any(d, self_kv(d), false, q, k, v, dout, lse, dk, dv, workspace,
+                  VD_STREAM(stream));
 }
 
 int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k, const void* v,
@@ -2003,6 +2134,47 @@ int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k, const 
   int rc = vd_attention_bwd_dq(d, q, k, v, o, dout, lse, dq, workspace, stream);
   if (rc) return rc;
   return vd_attention_bwd_dkdv(d, q, k, v, dout, lse, dk, dv, workspace, stream);
+}
+
+// ---- cross-attention: queries / output as vd_attn_desc, K/V rows of their own
+int vd_cross_attention_fwd(const vd_xattn_desc* x, const void* q, const void* k, const void* v,
+                           void* o, float* lse, void* workspace, size_t workspace_bytes,
+                           void* stream) {
+  int rc = check_xattn(x);
+  if (rc) return rc;
+  VD_REQUIRE(q && k && v && o && lse, "null tensor");
+  return fwd_any(&x->q, cross_kv(x), true, q, k, v, o, lse, workspace, workspace_bytes,
+                 VD_STREAM(stream));
+}
+
+size_t vd_cross_attention_fwd_workspace_size(const vd_xattn_desc* x) {
+  if (check_xattn(x)) return 0;
+  return fwd_ws_any(&x->q, x->kv_len, true);
+}
+
+size_t vd_cross_attention_bwd_workspace_size(const vd_xattn_desc* x) {
+  if (check_xattn(x)) return 0;
+  return bwd_ws_any(&x->q, x->kv_len, true);
+}
+
+int vd_cross_attention_bwd_dq(const vd_xattn_desc* x, const void* q, const void* k,
+                              const void* v, const void* o, const void* dout, const float* lse,
+                              void* dq, void* workspace, void* stream) {
+  int rc = check_xattn(x);
+  if (rc) return rc;
+  VD_REQUIRE(q && k && v && o && dout && lse && dq && workspace, "null tensor");
+  return dq_any(&x->q, cross_kv(x), true, q, k, v, o, dout, lse, dq, workspace,
+                VD_STREAM(stream));
+}
+
+int vd_cross_attention_bwd_dkdv(const vd_xattn_desc* x, const void* q, const void* k,
+                                const void* v, const void* dout, const float* lse, void* dk,
+                                void* dv, void* workspace, void* stream) {
+  int rc = check_xattn(x);
+  if (rc) return rc;
+  VD_REQUIRE(q && k && v && dout && lse && dk && dv && workspace, "null tensor");
+  return dkdv_any(&x->q, cross_kv(x), true, q, k, v, dout, lse, dk, dv, workspace,
+                  VD_STREAM(stream));
 }
 
 }  // extern "C"

@@ -39,6 +39,12 @@ class AttnDesc(C.Structure):
                 ("scale", _f), ("dtype", _i)]
 
 
+class XAttnDesc(C.Structure):
+    """vd_xattn_desc: queries / output as AttnDesc, K/V rows of their own."""
+    _fields_ = [("q", AttnDesc), ("kv_len", _i), ("kv_batch_stride", _i64),
+                ("kv_group_stride", _i64), ("kv_token_stride", _i64)]
+
+
 _SIGS = {
     "vd_version": (_i, []),
     "vd_last_error": (C.c_char_p, []),
@@ -78,6 +84,14 @@ _SIGS = {
                                  _vp]),
     "vd_attention_bwd_dkdv": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp]),
+    "vd_cross_attention_fwd_workspace_size": (_sz, [C.POINTER(XAttnDesc)]),
+    "vd_cross_attention_fwd": (_i, [C.POINTER(XAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _sz,
+                                    _vp]),
+    "vd_cross_attention_bwd_workspace_size": (_sz, [C.POINTER(XAttnDesc)]),
+    "vd_cross_attention_bwd_dq": (_i, [C.POINTER(XAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp]),
+    "vd_cross_attention_bwd_dkdv": (_i, [C.POINTER(XAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp,
+                                         _vp, _vp, _vp]),
     "vd_layernorm_workspace_size": (_sz, [_i, _i]),
     "vd_layernorm_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, C.c_float, _i, _vp]),
     "vd_layernorm_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _sz,

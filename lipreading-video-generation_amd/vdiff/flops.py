@@ -45,8 +45,9 @@ def _attn(w: Work, B, C, heads, T, HW, mode):
         _conv(w, B, T * HW, C, C, 1)
 
 
-def unet_forward_work(model, x_shape) -> Work:
-    """Walk a vdiff UNetModel for input shape [B, Cin, (T,) H, W]."""
+def unet_forward_work(model, x_shape, audio_tokens=12) -> Work:
+    """Walk a vdiff UNetModel for input shape [B, Cin, (T,) H, W] (audio cross-attention
+    branches, when present, onto `audio_tokens` wav2vec2 tokens per frame)."""
     from .nn import AttentionBlock, Downsample, ResBlock, Upsample
 
     B = x_shape[0]
@@ -69,6 +70,14 @@ def unet_forward_work(model, x_shape) -> Work:
             elif isinstance(layer, AttentionBlock):
                 _attn(w, B, layer.channels, layer.num_heads, T, state["H"] * state["W"],
                       layer.attention_mode)
+                if getattr(layer, "audio_attention", False):  # build extension
+                    C, HW = layer.channels, state["H"] * state["W"]
+                    L = audio_tokens if layer.audio_per_frame else T * audio_tokens
+                    nq = HW if layer.audio_per_frame else T * HW
+                    w.attn += 4.0 * B * (T * HW // nq) * nq * L * C
+                    _conv(w, B, T * HW, C, C, 1)              # audio_q
+                    _conv(w, B, T * HW, C, C, 1)              # audio_proj_out
+                    _conv(w, B * T, audio_tokens, 2 * C, layer.audio_kv.in_features, 1)
             elif isinstance(layer, Downsample):
                 state["H"] = (state["H"] + 1) // 2
                 state["W"] = (state["W"] + 1) // 2

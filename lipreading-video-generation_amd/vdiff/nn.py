@@ -159,11 +159,16 @@ class TimestepBlock(nn.Module):
 
 
 class TimestepEmbedSequential(nn.Sequential, TimestepBlock):
-    """unet.py:78-90."""
+    """unet.py:78-90; `context` (audio tokens, build extension) reaches the attention blocks."""
 
-    def forward(self, x, emb):
+    def forward(self, x, emb, context=None):
         for layer in self:
-            x = layer(x, emb) if isinstance(layer, TimestepBlock) else layer(x)
+            if isinstance(layer, TimestepBlock):
+                x = layer(x, emb)
+            elif context is not None and isinstance(layer, AttentionBlock):
+                x = layer(x, context=context)
+            else:
+                x = layer(x)
         return x
 
 
@@ -297,7 +302,8 @@ class AttentionBlock(nn.Module):
     """
 
     def __init__(self, channels, num_heads=1, num_head_channels=-1, use_checkpoint=False,
-                 use_new_attention_order=False, attention_mode="joint"):
+                 use_new_attention_order=False, attention_mode="joint", audio_attention=False,
+                 audio_context_dim=768, audio_per_frame=True):
         super().__init__()
         self.channels = channels
         if num_head_channels == -1:
@@ -319,9 +325,21 @@ class AttentionBlock(nn.Module):
             self.temporal_norm = normalization(channels)
             self.temporal_qkv = conv_nd(1, channels, channels * 3, 1)
             self.temporal_proj_out = zero_module(conv_nd(1, channels, channels, 1))
+        # audio cross-attention (north_star build extension; the reference conditions on audio
+        # by concatenation only, unet_audio.py:52-61): queries from the video tokens, keys /
+        # values from the audio tokens of the clip's frames, zero-initialised projection
+        self.audio_attention = audio_attention
+        self.audio_per_frame = audio_per_frame
+        if audio_attention:
+            self.audio_norm = normalization(channels)
+            self.audio_q = conv_nd(1, channels, channels, 1)
+            self.audio_kv = linear(audio_context_dim, 2 * channels)
+            self.audio_proj_out = zero_module(conv_nd(1, channels, channels, 1))
 
-    def forward(self, x):
-        return checkpoint(self._forward, (x,), self.parameters(), self.use_checkpoint)
+    def forward(self, x, context=None):
+        if context is None:
+            return checkpoint(self._forward, (x,), self.parameters(), self.use_checkpoint)
+        return checkpoint(self._forward, (x, context), self.parameters(), self.use_checkpoint)
 
     def _attend(self, xf, norm, qkv_conv, proj, mode, spatial):
         h = ops.group_norm_silu(xf, norm.weight, norm.bias, norm.num_groups, norm.eps, silu=False)
@@ -329,7 +347,16 @@ class AttentionBlock(nn.Module):
         a = ops.attention(qkv, self.num_heads, mode=mode, spatial=spatial, legacy=self.legacy)
         return ops.conv(a, proj.weight, proj.bias, residual=xf)
 
-    def _forward(self, x):
+    def _cross(self, h, context, frames):
+        """h + audio_proj_out(cross_attention(audio_q(GN(h)), audio_kv(audio tokens)))."""
+        a = ops.group_norm_silu(h, self.audio_norm.weight, self.audio_norm.bias,
+                                self.audio_norm.num_groups, self.audio_norm.eps, silu=False)
+        q = ops.conv(a, self.audio_q.weight, self.audio_q.bias)
+        kv = ops.linear(context.to(h.dtype), self.audio_kv.weight, self.audio_kv.bias)
+        o = ops.cross_attention(q, kv, self.num_heads, frames, self.audio_per_frame)
+        return ops.conv(o, self.audio_proj_out.weight, self.audio_proj_out.bias, residual=h)
+
+    def _forward(self, x, context=None):
         b, c, *spatial = x.shape
         x = ops.to_cl(x)
         xf = x.reshape(b, c, -1)
@@ -341,6 +368,8 @@ class AttentionBlock(nn.Module):
                              "temporal", sp)
         else:
             h = self._attend(xf, self.norm, self.qkv, self.proj_out, mode, sp)
+        if self.audio_attention and context is not None:
+            h = self._cross(h, context, sp[0])
         return h.reshape(b, c, *spatial)
 
 
@@ -379,7 +408,8 @@ class UNetModel(nn.Module):
                  dims=2, num_classes=None, use_checkpoint=False, use_fp16=False, num_heads=1,
                  num_head_channels=-1, num_heads_upsample=-1, use_scale_shift_norm=False,
                  resblock_updown=False, use_new_attention_order=False, *,
-                 attention_mode="joint", use_bf16=False):
+                 attention_mode="joint", use_bf16=False, audio_attention=False,
+                 audio_context_dim=768):
         super().__init__()
         if num_heads_upsample == -1:
             num_heads_upsample = num_heads
@@ -399,6 +429,7 @@ class UNetModel(nn.Module):
         self.num_head_channels = num_head_channels
         self.num_heads_upsample = num_heads_upsample
         self.attention_mode = attention_mode
+        self.audio_attention = audio_attention
         self.dims = dims
 
         time_embed_dim = model_channels * 4
@@ -416,7 +447,9 @@ class UNetModel(nn.Module):
             return AttentionBlock(ch, use_checkpoint=use_checkpoint, num_heads=nh,
                                   num_head_channels=num_head_channels,
                                   use_new_attention_order=use_new_attention_order,
-                                  attention_mode=attention_mode)
+                                  attention_mode=attention_mode,
+                                  audio_attention=audio_attention,
+                                  audio_context_dim=audio_context_dim)
 
         if resblock_updown:
             raise NotImplementedError("resblock_updown is not on the accelerated path")
@@ -466,7 +499,9 @@ class UNetModel(nn.Module):
     def convert_to_fp32(self):
         self.dtype = th.float32
 
-    def forward(self, x, timesteps, y=None):
+    def forward(self, x, timesteps, y=None, *, context=None):
+        """unet.py:646-675; `context` = audio tokens [B*T, L, F] for the audio
+        cross-attention branches (audio_attention=True, build extension)."""
         assert (y is not None) == (self.num_classes is not None), \
             "must specify y if and only if the model is class-conditional"
         hs = []
@@ -476,12 +511,12 @@ class UNetModel(nn.Module):
             emb = emb + self.label_emb(y)
         h = ops.to_cl(x.type(self.dtype))
         for module in self.input_blocks:
-            h = module(h, emb)
+            h = module(h, emb, context)
             hs.append(h)
-        h = self.middle_block(h, emb)
+        h = self.middle_block(h, emb, context)
         for module in self.output_blocks:
             h = _CatFn.apply(h, hs.pop())
-            h = module(h, emb)
+            h = module(h, emb, context)
         gn, conv = self.out[0], self.out[2]
         h = ops.group_norm_silu(h, gn.weight, gn.bias, gn.num_groups, gn.eps)
         h = ops.conv(h, conv.weight, conv.bias, conv.stride, conv.padding)

@@ -16,7 +16,7 @@ from typing import Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import AttnDesc, ConvDesc, VD_BF16, VD_F32
+from ._lib import AttnDesc, ConvDesc, VD_BF16, VD_F32, XAttnDesc
 
 _DT = {torch.float32: VD_F32, torch.bfloat16: VD_BF16}
 
@@ -720,6 +720,74 @@ class AttentionFn(torch.autograd.Function):
             if ev is not None:
                 _timer.end(ev, "attn_bwd_dkdv", d)
         return dqkv, None, None, None, None
+
+
+def _xattn_desc(B, T, HW, C, heads, L, dtype, per_frame):
+    """Cross-attention descriptor: video tokens of a channels-last [B][T][HW][C] buffer
+    (per frame: one sequence per (b, t, head); else one per (b, head) over all T*HW tokens)
+    attend to audio tokens of a [B*T][L][2C] buffer (k | v channel halves, head h at
+    channel offset h*ch of each half)."""
+    ch = C // heads
+    scale = 1.0 / math.sqrt(ch)
+    if per_frame:
+        q = AttnDesc(B * T * heads, HW, ch, heads, HW * C, ch, C, HW * C, ch, C, scale, dtype)
+        return XAttnDesc(q, L, L * 2 * C, ch, 2 * C)
+    q = AttnDesc(B * heads, T * HW, ch, heads, T * HW * C, ch, C, T * HW * C, ch, C, scale, dtype)
+    return XAttnDesc(q, T * L, T * L * 2 * C, ch, 2 * C)
+
+
+class CrossAttentionFn(torch.autograd.Function):
+    """softmax(q k^T / sqrt(ch)) v with q from the video tokens [B, C, T*HW] (channels-
+    last) and k | v from audio tokens [B*T, L, 2C] (vd_cross_attention_*)."""
+
+    @staticmethod
+    def forward(ctx, q, kv, heads: int, frames: int, per_frame: bool):
+        _gpu(q, kv)
+        q = to_cl(q)
+        B, C, N = q.shape
+        T = frames
+        if N % T or kv.shape[0] != B * T or kv.shape[2] != 2 * C:
+            raise ValueError(f"cross_attention: q {tuple(q.shape)} / kv {tuple(kv.shape)} / "
+                             f"frames {T} do not match")
+        kv = kv.to(q.dtype).contiguous()
+        dt = _DT[q.dtype]
+        x = _xattn_desc(B, T, N // T, C, heads, kv.shape[1], dt, per_frame)
+        out = empty_cl([B, C, N], q.dtype, q.device)
+        lse = torch.empty(x.q.nseq * x.q.seq_len, dtype=torch.float32, device=q.device)
+        nws = _lib.lib().vd_cross_attention_fwd_workspace_size(x)
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=q.device)
+        es = q.element_size()
+        _lib.call("vd_cross_attention_fwd", x, q.data_ptr(), kv.data_ptr(),
+                  kv.data_ptr() + C * es, out.data_ptr(), _p(lse), _p(ws), nws, _stream(q))
+        ctx.save_for_backward(q, kv, out, lse)
+        ctx.cfg = (heads, T, per_frame)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, kv, out, lse = ctx.saved_tensors
+        heads, T, per_frame = ctx.cfg
+        B, C, N = q.shape
+        dout = to_cl(dout).to(q.dtype)
+        x = _xattn_desc(B, T, N // T, C, heads, kv.shape[1], _DT[q.dtype], per_frame)
+        dq = empty_cl([B, C, N], q.dtype, q.device)
+        dkv = torch.empty_like(kv)
+        ws = torch.empty(max(1, _lib.lib().vd_cross_attention_bwd_workspace_size(x)),
+                         dtype=torch.uint8, device=q.device)
+        es, st = q.element_size(), _stream(q)
+        k, v = kv.data_ptr(), kv.data_ptr() + C * es
+        _lib.call("vd_cross_attention_bwd_dq", x, q.data_ptr(), k, v, out.data_ptr(),
+                  dout.data_ptr(), _p(lse), dq.data_ptr(), _p(ws), st)
+        _lib.call("vd_cross_attention_bwd_dkdv", x, q.data_ptr(), k, v, dout.data_ptr(), _p(lse),
+                  dkv.data_ptr(), dkv.data_ptr() + C * es, _p(ws), st)
+        return dq, dkv, None, None, None
+
+
+def cross_attention(q, kv, heads=1, frames=1, per_frame=True):
+    """Audio cross-attention (build extension, north_star): video tokens q [B, C, T*H*W]
+    (channels-last) attend to audio tokens kv [B*T, L, 2C] (k | v), per frame (frame t's
+    H*W tokens onto window t's L tokens) or over the whole clip (per_frame=False)."""
+    return CrossAttentionFn.apply(q, kv, heads, frames, bool(per_frame))
 
 
 ATTN_CONFIGS = {"auto": -1, "base": 0, "nb2": 1, "w8": 2, "p8": 3, "p4": 4, "d8": 5, "d8n": 6, "d4": 7}

@@ -11,6 +11,12 @@ the first conv's channels-last input.
 broadcast over T; one audio window per output frame ([B*T, samples] or pre-pooled
 features [B*T, F]) broadcast over (H, W).  With T = 1 / dims = 2 this is the
 reference computation.
+
+Audio cross-attention (north_star build extension, audio_attention=True): every attention
+block adds a cross-attention branch whose queries are the video tokens and whose keys /
+values are the (unpooled) wav2vec2 hidden states of the frame's audio window, 12 tokens
+per 4000-sample window (vdiff.nn.AttentionBlock, ops.cross_attention).  Off by default:
+the reference conditions by concatenation only.
 """
 from __future__ import annotations
 
@@ -75,14 +81,16 @@ class UNetAudio(UNetModel):
                  num_head_channels=-1, num_heads_upsample=-1, use_scale_shift_norm=False,
                  resblock_updown=False, use_new_attention_order=False, audio_feature_dim=512,
                  projected_audio_dim=256, *, attention_mode="joint", use_bf16=False,
-                 audio_encoder_pretrained=None, freeze_audio_encoder=False, audio_encoder=True):
+                 audio_encoder_pretrained=None, freeze_audio_encoder=False, audio_encoder=True,
+                 audio_attention=False):
         super().__init__(image_size,
                          in_channels + projected_audio_dim + (im_cond_output_ch if image_cond else 0),
                          model_channels, out_channels, num_res_blocks, attention_resolutions,
                          dropout, channel_mult, conv_resample, dims, num_classes, use_checkpoint,
                          use_fp16, num_heads, num_head_channels, num_heads_upsample,
                          use_scale_shift_norm, resblock_updown, use_new_attention_order,
-                         attention_mode=attention_mode, use_bf16=use_bf16)
+                         attention_mode=attention_mode, use_bf16=use_bf16,
+                         audio_attention=audio_attention, audio_context_dim=audio_feature_dim)
         self.audio_encoder = Wav2Vec2Encoder(pretrained=audio_encoder_pretrained) \
             if audio_encoder else None
         if self.audio_encoder is not None and freeze_audio_encoder:
@@ -97,28 +105,36 @@ class UNetAudio(UNetModel):
                                        out_channels=im_cond_output_ch, kernel_size=1, bias=False)
 
     def encode_audio(self, audio):
-        """wav2vec2 states mean-pooled over time: [B*T, F].  `audio` is the processor dict
-        ({'input_values': [B*T, samples]}) or already-pooled features [B*T, F] (lets a
-        sampler encode the audio once instead of at every step)."""
-        if isinstance(audio, dict) or (th.is_tensor(audio) and audio.shape[-1] !=
-                                       self.audio_transformer.transform[0].in_features):
-            if self.audio_encoder is None:
-                raise ValueError("model built without an audio encoder: pass pooled features")
-            if (self.dtype == th.bfloat16 and next(self.audio_encoder.parameters()).is_cuda
-                    and os.environ.get("VDIFF_W2V_BF16")):
-                # opt-in bf16 wav2vec2 (SURVEY 8f rank 2): GEMMs / convs under autocast, fp32
-                # master weights and pooled output.  Off by default: same-box A/B of the
-                # train step measured 427-429 ms with it against 423-424 without (MIOpen's
-                # bf16 convolutions for the feature extractor are slower than its fp32 ones)
-                with th.autocast("cuda", dtype=th.bfloat16):
-                    return self.audio_encoder(audio).float().mean(dim=1)
-            return self.audio_encoder(audio).mean(dim=1)
-        return audio
+        """wav2vec2 states of each audio window: mean-pooled over time, [B*T, F] -- or, with
+        audio_attention, the tokens themselves [B*T, L, F] (their mean is the pooled vector).
+        `audio` is the processor dict ({'input_values': [B*T, samples]}) or already-encoded
+        features / tokens (lets a sampler encode the audio once instead of at every step)."""
+        F_ = self.audio_transformer.transform[0].in_features
+        if th.is_tensor(audio) and audio.shape[-1] == F_:
+            return audio
+        if self.audio_encoder is None:
+            raise ValueError("model built without an audio encoder: pass encoded features")
+        if (self.dtype == th.bfloat16 and next(self.audio_encoder.parameters()).is_cuda
+                and os.environ.get("VDIFF_W2V_BF16")):
+            # opt-in bf16 wav2vec2 (SURVEY 8f rank 2): GEMMs / convs under autocast, fp32
+            # master weights and pooled output.  Off by default: same-box A/B of the
+            # train step measured 427-429 ms with it against 423-424 without (MIOpen's
+            # bf16 convolutions for the feature extractor are slower than its fp32 ones)
+            with th.autocast("cuda", dtype=th.bfloat16):
+                tokens = self.audio_encoder(audio).float()
+        else:
+            tokens = self.audio_encoder(audio)
+        return tokens if self.audio_attention else tokens.mean(dim=1)
 
     def forward(self, image, cond_image, audio, timesteps, y=None):
         B = image.shape[0]
         T = image.shape[2] if image.dim() == 5 else 1
-        feats = self.encode_audio(audio).float()
+        enc = self.encode_audio(audio).float()
+        tokens = enc if enc.dim() == 3 else None
+        if self.audio_attention and tokens is None:
+            raise ValueError("audio_attention needs the audio tokens [B*T, L, F], not pooled "
+                             "features")
+        feats = tokens.mean(dim=1) if tokens is not None else enc
         a = self.audio_transformer(feats).reshape(B, T, self.projected_audio_dim)
         if self.image_cond:
             imc = self.cond_conv_in(cond_image.type(self.dtype) if cond_image.dim() == 4
@@ -126,9 +142,10 @@ class UNetAudio(UNetModel):
         else:
             imc = image.new_zeros(B, 0, 1, 1)
         x = ops.cond_concat(image.type(self.dtype), imc, a, cpad=(self.in_channels + 7) // 8 * 8)
-        return self._unet_forward_padded(x, timesteps, y, image.dtype)
+        ctx = tokens if self.audio_attention else None
+        return self._unet_forward_padded(x, timesteps, y, image.dtype, ctx)
 
-    def _unet_forward_padded(self, x, timesteps, y, out_dtype):
+    def _unet_forward_padded(self, x, timesteps, y, out_dtype, context=None):
         # The concat buffer carries zero padding channels up to a multiple of 8; the
         # first conv's weight is zero-extended to match (same result as the reference
         # 195-channel conv, no extra pad copy).
@@ -144,13 +161,13 @@ class UNetAudio(UNetModel):
         h = ops.conv(x, w, first.bias, first.stride, first.padding)
         hs.append(h)
         for module in list(self.input_blocks)[1:]:
-            h = module(h, emb)
+            h = module(h, emb, context)
             hs.append(h)
-        h = self.middle_block(h, emb)
+        h = self.middle_block(h, emb, context)
         from .nn import _CatFn
         for module in self.output_blocks:
             h = _CatFn.apply(h, hs.pop())
-            h = module(h, emb)
+            h = module(h, emb, context)
         gn, conv = self.out[0], self.out[2]
         h = ops.group_norm_silu(h, gn.weight, gn.bias, gn.num_groups, gn.eps)
         h = ops.conv(h, conv.weight, conv.bias, conv.stride, conv.padding)

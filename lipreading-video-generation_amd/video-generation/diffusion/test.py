@@ -73,6 +73,7 @@ def load_model_and_scheduler(config, *, seed=0):
         dims=lp.get("dims", 2),
         attention_mode=lp.get("attention_mode", "joint"),
         use_bf16=lp.get("dtype", "bf16") == "bf16",
+        audio_attention=lp.get("audio_attention", False),
         # with a checkpoint the wav2vec2 weights come from it; without one the random
         # encoder is the explicitly requested smoke mode
         audio_encoder_pretrained=False)
@@ -145,6 +146,8 @@ def parse(argv=None):
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--image-size", type=int, default=config["dataset_params"]["im_size"])
     ap.add_argument("--attention-mode", default="joint")
+    ap.add_argument("--audio-attention", action="store_true",
+                    help="audio cross-attention branches (build extension)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--out-dir", default=OUT_DIR)
     ap.add_argument("--cond-npz", default=None)
@@ -166,7 +169,7 @@ def main(argv=None):
     cfg = {k: dict(v) for k, v in config.items()}
     cfg["dataset_params"]["im_size"] = args.image_size
     cfg["ldm_params"].update(dims=args.dims, attention_mode=args.attention_mode,
-                             dtype=args.dtype)
+                             dtype=args.dtype, audio_attention=args.audio_attention)
     cfg["train_params"]["ldm_ckpt_name"] = args.ckpt
     config.update(cfg)
     model, scheduler = load_model_and_scheduler(config, seed=args.seed)

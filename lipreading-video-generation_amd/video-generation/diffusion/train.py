@@ -52,6 +52,9 @@ def parse(argv=None):
     ap.add_argument("--num-timesteps", type=int, default=100)
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--freeze-audio-encoder", action="store_true")
+    ap.add_argument("--audio-attention", action="store_true",
+                    help="audio cross-attention branches in every attention block (build "
+                         "extension; the reference conditions by concatenation only)")
     ap.add_argument("--ckpt", default="best_diffusion.pth")
     ap.add_argument("--resume", default=None, help="checkpoint with model/optimizer/step")
     ap.add_argument("--seed", type=int, default=0)
@@ -71,6 +74,7 @@ def build_model(args):
                      dims=args.dims, audio_feature_dim=768, projected_audio_dim=128,
                      use_bf16=args.dtype == "bf16", attention_mode=args.attention_mode,
                      freeze_audio_encoder=args.freeze_audio_encoder,
+                     audio_attention=args.audio_attention,
                      # True: the pretrained weights must load (raises when absent);
                      # False: architecture only (random init, or weights from --resume)
                      audio_encoder_pretrained=not (args.random_audio_encoder or args.resume))

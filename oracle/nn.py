@@ -76,6 +76,44 @@ def qkv_attention(qkv: torch.Tensor, heads: int, legacy: bool = True, mode: str 
     return ungroup(a).reshape(B, heads * ch, N)
 
 
+def cross_attention(q: torch.Tensor, kv: torch.Tensor, heads: int = 1, frames: int = 1,
+                    per_frame: bool = True) -> torch.Tensor:
+    """Audio cross-attention (build extension of the north star; the reference conditions on
+    audio by concatenation only, unet_audio.py:52-61, so this is pinned by no reference
+    output): video tokens q [B, C, T*HW] attend to audio tokens kv [B*T, L, 2C] (k | v
+    channel halves; head h at channel offset h*ch), softmax(q k^T / sqrt(ch)) v -- the
+    QKVAttention math (unet.py:388-401) with separate key/value tokens."""
+    B, C, N = q.shape
+    T, L, ch = frames, kv.shape[1], C // heads
+    HW = N // T
+    k, v = kv[..., :C], kv[..., C:]
+    if per_frame:
+        qs = q.reshape(B, heads, ch, T, HW).permute(0, 3, 1, 4, 2).reshape(B * T * heads, HW, ch)
+
+        def kvs(u):
+            return u.reshape(B * T, L, heads, ch).permute(0, 2, 1, 3).reshape(B * T * heads, L, ch)
+    else:
+        qs = q.reshape(B, heads, ch, N).permute(0, 1, 3, 2).reshape(B * heads, N, ch)
+
+        def kvs(u):
+            return u.reshape(B, T * L, heads, ch).permute(0, 2, 1, 3).reshape(B * heads, T * L, ch)
+    w = torch.softmax((qs @ kvs(k).transpose(1, 2)).float() / math.sqrt(ch), dim=-1)
+    o = w.to(qs.dtype) @ kvs(v)
+    if per_frame:
+        return o.reshape(B, T, heads, HW, ch).permute(0, 2, 4, 1, 3).reshape(B, C, N)
+    return o.reshape(B, heads, N, ch).permute(0, 1, 3, 2).reshape(B, C, N)
+
+
+def audio_cross_block(P, pre, h, context, heads=1, frames=1, per_frame=True):
+    """The AttentionBlock's audio cross-attention residual branch (build extension):
+    h + audio_proj_out(cross_attention(audio_q(GN(h)), audio_kv(context)))."""
+    a = group_norm(h, P[pre + "audio_norm.weight"], P[pre + "audio_norm.bias"])
+    q = conv(a, P[pre + "audio_q.weight"], P[pre + "audio_q.bias"])
+    kv = linear(context, P[pre + "audio_kv.weight"], P[pre + "audio_kv.bias"])
+    o = cross_attention(q, kv, heads, frames, per_frame)
+    return h + conv(o, P[pre + "audio_proj_out.weight"], P[pre + "audio_proj_out.bias"])
+
+
 def upsample(x, dims):
     """Upsample.forward (unet.py:112-122), nearest; dims=3 keeps T."""
     if dims == 3:
@@ -101,11 +139,14 @@ def resblock(P, pre, x, emb, dropout_mask=None):
     return x + h
 
 
-def attention_block(P, pre, x, heads=1, legacy=True, mode="joint"):
+def attention_block(P, pre, x, heads=1, legacy=True, mode="joint", context=None,
+                    per_frame=True):
     """AttentionBlock._forward (unet.py:311-317).
 
     mode "spatial_temporal" (build extension): the reference block over per-frame token
-    groups, then a second one over per-pixel groups with the temporal_* parameters."""
+    groups, then a second one over per-pixel groups with the temporal_* parameters.
+    context (build extension): audio tokens [B*T, L, F] for the audio_* cross-attention
+    branch, applied after the self-attention when the block has audio_* parameters."""
     B, C = x.shape[:2]
     spatial = list(x.shape[2:])
     sp = spatial if len(spatial) == 3 else [1] + spatial
@@ -121,6 +162,8 @@ def attention_block(P, pre, x, heads=1, legacy=True, mode="joint"):
         h = attend(attend(xf, "", "spatial"), "temporal_", "temporal")
     else:
         h = attend(xf, "", mode)
+    if context is not None and pre + "audio_q.weight" in P:
+        h = audio_cross_block(P, pre, h, context, heads, sp[0], per_frame)
     return h.reshape(x.shape)
 
 

@@ -21,7 +21,7 @@ from . import nn as onn
 def build_plan(in_channels, model_channels, out_channels, num_res_blocks, attention_resolutions,
                channel_mult=(1, 2, 4, 8), dims=2, num_heads=1, num_head_channels=-1,
                num_heads_upsample=-1, conv_resample=True, use_new_attention_order=False,
-               attention_mode="joint"):
+               attention_mode="joint", audio_attention=0):
     """Layer specs per block, as UNetModel.__init__ builds them (unet.py:476-628)."""
     if num_heads_upsample == -1:
         num_heads_upsample = num_heads
@@ -63,7 +63,7 @@ def build_plan(in_channels, model_channels, out_channels, num_res_blocks, attent
     return {"input_blocks": inputs, "middle_block": middle, "output_blocks": outputs,
             "model_channels": model_channels, "first_ch": first, "out_channels": out_channels,
             "dims": dims, "legacy": not use_new_attention_order, "conv_resample": conv_resample,
-            "attention_mode": attention_mode}
+            "attention_mode": attention_mode, "audio_attention": audio_attention}
 
 
 def _k(dims, k):
@@ -115,6 +115,16 @@ def param_shapes(plan) -> "OrderedDict[str, tuple]":
                 S[pre + "temporal_qkv.bias"] = (3 * c,)
                 S[pre + "temporal_proj_out.weight"] = (c, c, 1)
                 S[pre + "temporal_proj_out.bias"] = (c,)
+            fa = plan.get("audio_attention", 0)  # audio token width; 0 = no cross-attention
+            if fa:
+                S[pre + "audio_norm.weight"] = (c,)
+                S[pre + "audio_norm.bias"] = (c,)
+                S[pre + "audio_q.weight"] = (c, c, 1)
+                S[pre + "audio_q.bias"] = (c,)
+                S[pre + "audio_kv.weight"] = (2 * c, fa)
+                S[pre + "audio_kv.bias"] = (2 * c,)
+                S[pre + "audio_proj_out.weight"] = (c, c, 1)
+                S[pre + "audio_proj_out.bias"] = (c,)
         elif kind == "down":
             S[pre + "op.weight"] = (spec[1], spec[1]) + _k(d, 3)
             S[pre + "op.bias"] = (spec[1],)
@@ -165,7 +175,7 @@ def init_params(shapes, seed: int = 1234) -> dict:
     return P
 
 
-def _run_block(P, pre, blk, h, emb, plan, attn_mode):
+def _run_block(P, pre, blk, h, emb, plan, attn_mode, context=None):
     d = plan["dims"]
     for j, spec in enumerate(blk):
         lp = f"{pre}{j}."
@@ -176,7 +186,7 @@ def _run_block(P, pre, blk, h, emb, plan, attn_mode):
             h = onn.resblock(P, lp, h, emb)
         elif kind == "attn":
             h = onn.attention_block(P, lp, h, heads=spec[2], legacy=plan["legacy"],
-                                    mode=attn_mode)
+                                    mode=attn_mode, context=context)
         elif kind == "down":
             h = onn.downsample_block(P, lp, h, d)
         elif kind == "up":
@@ -184,8 +194,9 @@ def _run_block(P, pre, blk, h, emb, plan, attn_mode):
     return h
 
 
-def unet_forward(P, plan, x, timesteps, attn_mode=None):
-    """UNetModel.forward (unet.py:646-675), no class conditioning."""
+def unet_forward(P, plan, x, timesteps, attn_mode=None, context=None):
+    """UNetModel.forward (unet.py:646-675), no class conditioning; `context` = audio tokens
+    for the audio cross-attention branches (build extension)."""
     mc = plan["model_channels"]
     attn_mode = attn_mode or plan.get("attention_mode", "joint")
     e = onn.timestep_embedding(timesteps, mc)
@@ -194,12 +205,12 @@ def unet_forward(P, plan, x, timesteps, attn_mode=None):
     hs = []
     h = x.float()
     for i, blk in enumerate(plan["input_blocks"]):
-        h = _run_block(P, f"input_blocks.{i}.", blk, h, emb, plan, attn_mode)
+        h = _run_block(P, f"input_blocks.{i}.", blk, h, emb, plan, attn_mode, context)
         hs.append(h)
-    h = _run_block(P, "middle_block.", plan["middle_block"], h, emb, plan, attn_mode)
+    h = _run_block(P, "middle_block.", plan["middle_block"], h, emb, plan, attn_mode, context)
     for i, blk in enumerate(plan["output_blocks"]):
         h = torch.cat([h, hs.pop()], dim=1)
-        h = _run_block(P, f"output_blocks.{i}.", blk, h, emb, plan, attn_mode)
+        h = _run_block(P, f"output_blocks.{i}.", blk, h, emb, plan, attn_mode, context)
     h = onn.group_norm(h, P["out.0.weight"], P["out.0.bias"], silu=True)
     return onn.conv(h, P["out.2.weight"], P["out.2.bias"], padding=1)
 

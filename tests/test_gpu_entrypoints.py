@@ -80,3 +80,15 @@ print("OK", type(scheduler).__name__)
                          text=True, timeout=900)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     assert "OK LinearNoiseSchedulerV2" in out.stdout
+
+
+def test_sampling_entry_with_audio_cross_attention(tmp_path):
+    """test.py --audio-attention: the wav2vec2 tokens (not pooled) reach the cross-attention
+    branches of every attention block (build extension)."""
+    out_dir = tmp_path / "imgs"
+    _run("test.py", ["--dims", "3", "--frames", "2", "--image-size", "32", "--sampler", "ddim",
+                     "--steps", "2", "--save-every", "1", "--out-dir", str(out_dir),
+                     "--random-init", "--audio-attention"], tmp_path)
+    files = sorted(p for p in os.listdir(out_dir) if p.endswith(".npy"))
+    x0 = np.load(out_dir / files[0])
+    assert x0.shape == (1, 3, 2, 32, 32) and np.isfinite(x0).all()

@@ -35,3 +35,5 @@ def test_version_and_error_channel():
 def test_structs_match_header():
     assert ctypes.sizeof(_lib.ConvDesc) == 21 * 4
     assert ctypes.sizeof(_lib.AttnDesc) == 4 * 4 + 6 * 8 + 4 + 4
+    # vd_xattn_desc: the query descriptor, int kv_len (+4 padding), three int64 strides
+    assert ctypes.sizeof(_lib.XAttnDesc) == ctypes.sizeof(_lib.AttnDesc) + 8 + 3 * 8

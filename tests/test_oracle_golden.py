@@ -193,3 +193,28 @@ def test_one_adam_train_step():
     for k in names:
         assert rel_l2(grads[k], g["grad_" + k]) < 1e-4, k
         assert adam_delta_close(deltas[k], g["delta_" + k], g["grad_" + k]) < 1e-6, k
+
+
+def test_cross_attention_oracle_reduces_to_reference():
+    """Pins oracle.nn.cross_attention (the audio cross-attention restatement, no reference
+    counterpart) to the reference's attention math: with each frame's own k / v tokens as
+    the "audio" tokens it must equal QKVAttention (new order, unet.py:388-401) applied per
+    frame, whose output the golden blocks pin (abn_*, spatial regrouping st_spatial)."""
+    B, C, heads, T, HW = 2, 64, 2, 3, 20
+    qkv = seeded((B, 3 * C, T * HW), 90)
+    ref = onn.qkv_attention(qkv, heads, legacy=False, mode="spatial", spatial=(T, HW, 1))
+    q, k, v = qkv.chunk(3, dim=1)                                   # [B, C, T*HW] each
+    toks = lambda u: u.reshape(B, C, T, HW).permute(0, 2, 3, 1).reshape(B * T, HW, C)
+    kv = torch.cat([toks(k), toks(v)], dim=-1)                      # [B*T, HW, 2C]
+    out = onn.cross_attention(q, kv, heads, T, per_frame=True)
+    assert rel_l2(out, ref) < 1e-6
+    # clip level == joint attention
+    refj = onn.qkv_attention(qkv, heads, legacy=False, mode="joint")
+    outj = onn.cross_attention(q, kv, heads, T, per_frame=False)
+    assert rel_l2(outj, refj) < 1e-6
+    g = golden("blocks.npz")  # the reference QKVAttentionLegacy regrouped per frame
+    qkv2 = seeded((2, 3 * 64, 3 * 36), 46)
+    q2, k2, v2 = qkv2.chunk(3, dim=1)
+    tk = lambda u: u.reshape(2, 64, 3, 36).permute(0, 2, 3, 1).reshape(6, 36, 64)
+    out2 = onn.cross_attention(q2, torch.cat([tk(k2), tk(v2)], -1), 1, 3, per_frame=True)
+    assert rel_l2(out2, g["st_spatial"]) < 1e-5
