@@ -285,6 +285,35 @@ int vd_cross_attention_bwd_dkdv(const vd_xattn_desc* x, const void* q, const voi
                                 const void* v, const void* dout, const float* lse,
                                 void* dk, void* dv, void* workspace, void* stream);
 
+/* ---- data path (video-generation/dataset.py:68-139) ----------------
+ * Frames: the reference's ToPILImage -> Resize((S, S)) -> ToTensor -> Normalize(0.5, 0.5)
+ * (train.py:70-75, dataset.py:109-111) = PIL's antialiased bilinear resample.
+ * vd_resize_plan (HOST, no GPU) computes one axis of PIL's plan (libImaging/Resample.c
+ * precompute_coeffs + normalize_coeffs_8bpc): bounds int[out][2] (first tap, taps) and
+ * 22-bit fixed-point coefficients int[out][ksize], ksize = 2 * ceil(in / out) + 1 (<= cap).
+ * vd_frames_resize_normalize (GPU): uint8 frames [n][H][W][3] -> horizontal pass into tmp
+ * (uint8 [n][H][OW][3]) -> vertical pass -> (v / 255 - 0.5) / 0.5 in `dtype`, frame f at
+ * out + f * frame_stride as [3][OH][OW] (channels_last = 0) or [OH][OW][3]; the uint8
+ * values equal PIL's bit for bit.  Plans are device int arrays. */
+int vd_resize_plan(int in_size, int out_size, int* bounds, int* coef, int ksize_cap);
+int vd_frames_resize_normalize(const uint8_t* frames, int64_t n, int H, int W, int OH, int OW,
+                               const int* xbounds, const int* xcoef, int xksize,
+                               const int* ybounds, const int* ycoef, int yksize, uint8_t* tmp,
+                               void* out, int dtype, int64_t frame_stride, int channels_last,
+                               void* stream);
+/* HOST (no GPU): the audio window of one output frame, dataset.py:113-130 -- samples
+ * [int(sr * max(0, (out_frame - buffer_frames) / fps)), int(sr * out_frame / fps)) of the
+ * track wave fp32 [channels][n]; torchaudio highpass_biquad(300 Hz, Q 0.707) with lfilter's
+ * clamp to [-1, 1]; (x - mean) / std (unbiased, all channels); process_audio (:51-66):
+ * resample to target_sr (bug_compatible = 1: from orig_freq = channels, as the reference's
+ * size(0) comparison does; 0: from sr, identity when sr == target_sr; torchaudio's
+ * sinc_interp_hann kernel, width 6, rolloff 0.99), zero-pad / trim to target_len; then the
+ * Wav2Vec2 processor's (x - mean) / sqrt(var + 1e-7) per channel.  out fp32
+ * [channels][target_len]. */
+int vd_audio_window(const float* wave, int channels, int64_t n, int sr, double fps,
+                    int out_frame, int buffer_frames, int target_len, int target_sr,
+                    int bug_compatible, float* out);
+
 /* ---- ViViT lipreading encoder ops (lipreading/huggingface_vivit_model.py:18-33
  * over transformers' VivitModel: VivitLayer.layernorm_before/_after, final layernorm, VivitMLP
  * with hidden_act "gelu_fast").

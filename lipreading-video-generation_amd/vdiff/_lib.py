@@ -92,6 +92,10 @@ _SIGS = {
                                        _vp, _vp]),
     "vd_cross_attention_bwd_dkdv": (_i, [C.POINTER(XAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp]),
+    "vd_resize_plan": (_i, [_i, _i, _vp, _vp, _i]),
+    "vd_frames_resize_normalize": (_i, [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i,
+                                        _vp, _vp, _i, _i64, _i, _vp]),
+    "vd_audio_window": (_i, [_vp, _i, _i64, _i, C.c_double, _i, _i, _i, _i, _i, _vp]),
     "vd_layernorm_workspace_size": (_sz, [_i, _i]),
     "vd_layernorm_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, C.c_float, _i, _vp]),
     "vd_layernorm_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _sz,

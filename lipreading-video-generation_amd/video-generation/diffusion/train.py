@@ -35,6 +35,12 @@ from unet_audio import UNetAudio
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--synthetic", action="store_true", default=True)
+    ap.add_argument("--data", default=None,
+                    help="frame index (JSON lines, vdiff.data) over .vdclip files: real clips "
+                         "instead of synthetic ones")
+    ap.add_argument("--fix-audio-resample", action="store_true",
+                    help="resample audio from the track's rate (the reference resamples from "
+                         "orig_freq = channel count, dataset.py:53)")
     ap.add_argument("--dims", type=int, default=2, help="2 = reference per-frame, 3 = UNet3D")
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--image-size", type=int, default=128)
@@ -107,13 +113,24 @@ def train(argv=None):
         print(f"Training on {device} x{world}: {sum(p.numel() for p in model.parameters()) / 1e6:.1f}"
               f" M params, dims={args.dims}, {args.attention_mode} attention, {args.dtype}")
     frames = args.frames if args.dims == 3 else 1
+    batcher = None
+    if args.data:
+        from vdiff.data import ClipBatcher, load_frame_items
+        items = load_frame_items(args.data)
+        # DistributedSampler-equivalent: each rank draws from its own seed
+        batcher = ClipBatcher(items, args.batch_size, frames, args.num_timesteps, device,
+                              size=args.image_size, seed=args.seed * world + rank,
+                              bug_compatible=not args.fix_audio_resample, dims=args.dims)
     loss = torch.zeros(())
     for epoch in range(start_epoch, args.epochs):
         t0 = time.time()
         for step in range(args.steps_per_epoch):
-            clip = synthetic_clip(args.batch_size, frames, args.image_size, args.num_timesteps,
-                                  device, seed=(epoch * 1000003 + step) * world + rank,
-                                  dims=args.dims)
+            if batcher is not None:
+                clip = batcher.next()
+            else:
+                clip = synthetic_clip(args.batch_size, frames, args.image_size,
+                                      args.num_timesteps, device,
+                                      seed=(epoch * 1000003 + step) * world + rank, dims=args.dims)
             loss = trainer.step(clip)
         if rank == 0:
             dt = time.time() - t0
