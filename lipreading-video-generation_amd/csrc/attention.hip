@@ -410,7 +410,7 @@ __device__ __forceinline__ uint32_t seq_bytes(int n, int64_t ts, int D, int esz)
 // Runs body(t, tileA, tileB) over all 64-row tiles of two row streams (a, b) of one
 // sequence; with RC, the fp32 row constants rc0/rc1 of the tile are staged too and
 // passed as body's fourth argument (float* [rc0 64 | rc1 64]).
-template <typename T, int D, bool RC, int NW, typename Body>
+template <typename T, int D, bool RC, int NW, int NSTO = 0, typename Body>
 __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, int64_t ts_a,
                                           int64_t ts_b, const float* rc0, const float* rc1, int n,
                                           int tid, Body&& body) {
@@ -419,7 +419,7 @@ __device__ __forceinline__ void tile_loop(char* smem, const T* a, const T* b, in
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntiles = (n + kTile - 1) / kTile;
   if constexpr (kDMA<T>) {
-    constexpr int NST = nstage<D>();
+    constexpr int NST = NSTO ? NSTO : nstage<D>();  // NSTO: ring stages override
     constexpr int STAGE_BYTES = 2 * TE * 2 + (RC ? 768 : 0);
     constexpr int PER_TILE = 2 * dma_ipw<D, NW>() + (RC ? 1 : 0);
     const auto ra = make_rsrc(a, seq_bytes(n, ts_a, D, 2));
@@ -640,9 +640,10 @@ constexpr size_t tile_pipe_lds() { return 4 * (size_t)pipe_stage_bytes<D, RC, TR
 template <int D, int NW> constexpr int pipe_tr() { return D == 64 && NW == 8 ? VD_PIPE_TR : kTile; }
 
 
-template <typename T, int D, bool RC>
+template <typename T, int D, bool RC, int NSTO = 0>
 size_t tile_loop_lds() {
-  if constexpr (kDMA<T>) return (size_t)nstage<D>() * (2 * tile_elems<T, D>() * 2 + (RC ? 768 : 0));
+  if constexpr (kDMA<T>)
+    return (size_t)(NSTO ? NSTO : nstage<D>()) * (2 * tile_elems<T, D>() * 2 + (RC ? 768 : 0));
   else return 2 * tile_elems<T, D>() * sizeof(T) + (RC ? 512 : 0);
 }
 
@@ -1146,6 +1147,126 @@ __global__ void attn_dkdv_sum_kernel(const float* __restrict__ part, int splits,
     const int seq = (int)(row / nkv), tok = (int)(row % nkv);
     T* dst = (c8 < D ? dk + c8 : dv + (c8 - D)) + ka(seq) + (int64_t)tok * kts;
     store8(dst, acc);
+  }
+}
+
+// ================================================================== backward: dK, dV, paired
+// head_dim 128 with two waves per SIMD.  The 4-wave kernel above holds 32 keys' K and V
+// fragments (64 VGPRs) and their full dK^T / dV^T accumulators (128 VGPRs) per wave, so it
+// runs one wave per SIMD and nothing hides the S -> exp -> dV/dK dependency chain.  Here a
+// workgroup of 8 waves owns 128 keys: K (pre-scaled by scale*log2 e) and V of those keys sit
+// in LDS for the whole launch (64 KiB, read as the B operand exactly as the query tiles are
+// read as the A operand), and the SIMD partners w and w + 4 share one 32-key group: wave w
+// takes query rows 0-31 of every 64-row tile, wave w + 4 rows 32-63.  Each wave keeps its
+// own fp32 dK^T / dV^T partials (same products, half the queries each); the partners' sums
+// are added through LDS at the end.  Two ring stages (64 KiB + the resident K/V fit in 160).
+template <int D>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ nlse2,
+    const float* __restrict__ ndelta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int n,
+    SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale, KvAddr kv) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KEYS = 128, GTE = 32 * D;  // keys per workgroup; bf16 per 32-key group
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, kg = wave & 3, half = wave >> 2;
+  const int seq = blockIdx.y;
+  const int kw0 = blockIdx.x * KEYS;  // first key of the workgroup
+  const int64_t base = qa(seq), obase = oa(seq), kb = kv.a(seq);
+  bf16_t* kl = reinterpret_cast<bf16_t*>(smem);  // [4 groups][32 keys][D], tile swizzle
+  bf16_t* vl = kl + 4 * GTE;
+  char* ring = smem + 8 * GTE * 2;
+  // stage the workgroup's K (scaled) and V rows: 16 B per thread per step
+  {
+    const float c = scale * kLog2e;
+    constexpr int CPR = D / 8;
+    for (int i = tid; i < KEYS * CPR; i += 512) {
+      const int r = i / CPR, cc = i % CPR, key = kw0 + r;
+      uint4 kk = make_uint4(0, 0, 0, 0), vv = kk;
+      if (key < kv.n) {
+        kk = *reinterpret_cast<const uint4*>(k + kb + (int64_t)key * kv.ts + cc * 8);
+        vv = *reinterpret_cast<const uint4*>(v + kb + (int64_t)key * kv.ts + cc * 8);
+      }
+      const uint32_t in[4] = {kk.x, kk.y, kk.z, kk.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = pack2bf(__uint_as_float(in[e] << 16) * c, __uint_as_float(in[e] & 0xffff0000u) * c);
+      const int off = (r >> 5) * GTE + toff<bf16_t, D>(r & 31, cc * 8);
+      *reinterpret_cast<uint4*>(kl + off) = make_uint4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<uint4*>(vl + off) = vv;
+    }
+  }
+  __syncthreads();
+  const bf16_t* kgl = kl + kg * GTE;
+  const bf16_t* vgl = vl + kg * GTE;
+  f32x16 adv[D / 32], adk[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) adv[i] = adk[i] = f32x16{};
+  const int row0 = 32 * half;
+#ifdef VD_PAIR_PRIO
+  if (half) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for the second half
+#endif
+
+  tile_loop<bf16_t, D, true, 8, 2>(ring, q + base, dout + obase, ts, ots,
+                                   nlse2 + (int64_t)seq * n, ndelta + (int64_t)seq * n, n, tid,
+                                   [&](int, const bf16_t* Qt, const bf16_t* Ot, const float* L) {
+    f32x16 s, dp;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // registers 4g..4g+3 = query rows 8g + 4hh + 0..3
+      const float4 ls = *reinterpret_cast<const float4*>(L + row0 + 8 * g + 4 * hh);
+      const float4 dl = *reinterpret_cast<const float4*>(L + 64 + row0 + 8 * g + 4 * hh);
+      s[4 * g + 0] = ls.x; s[4 * g + 1] = ls.y; s[4 * g + 2] = ls.z; s[4 * g + 3] = ls.w;
+      dp[4 * g + 0] = dl.x; dp[4 * g + 1] = dl.y; dp[4 * g + 2] = dl.z; dp[4 * g + 3] = dl.w;
+    }
+    const int r = row0 + (lane & 31);
+#pragma unroll
+    for (int ss = 0; ss < D / 16; ++ss) {  // S'[q][key] - lse', dP[q][key] - delta
+      const bf16x8 qa8 = *reinterpret_cast<const bf16x8*>(Qt + toff<bf16_t, D>(r, 16 * ss + 8 * hh));
+      const bf16x8 kb8 = *reinterpret_cast<const bf16x8*>(kgl + toff<bf16_t, D>(lane & 31, 16 * ss + 8 * hh));
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa8, kb8, s, 0, 0, 0);
+      const bf16x8 oa8 = *reinterpret_cast<const bf16x8*>(Ot + toff<bf16_t, D>(r, 16 * ss + 8 * hh));
+      const bf16x8 vb8 = *reinterpret_cast<const bf16x8*>(vgl + toff<bf16_t, D>(lane & 31, 16 * ss + 8 * hh));
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa8, vb8, dp, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float pv = fast_exp2(s[e]);
+      s[e] = pv;
+      dp[e] *= pv;  // dS
+    }
+    const XOp<bf16_t> pp(s), ds(dp);
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) {
+      mma_tr<bf16_t, D>(adv[i], Ot, row0, 32 * i, pp, lane);  // dV^T += dO^T P
+      mma_tr<bf16_t, D>(adk[i], Qt, row0, 32 * i, ds, lane);  // dK^T += Q^T dS
+    }
+  });
+  // partner sums: waves 4-7 hand their partials to waves 0-3 through LDS (lane-interleaved,
+  // conflict-free); the ring and the K/V area are free once every wave left the loop
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem) + (int64_t)kg * (2 * D / 32) * 16 * 64;
+  if (half) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        red[((2 * i) * 16 + e) * 64 + lane] = adk[i][e];
+        red[((2 * i + 1) * 16 + e) * 64 + lane] = adv[i][e];
+      }
+  }
+  __syncthreads();
+  if (!half) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        adk[i][e] += red[((2 * i) * 16 + e) * 64 + lane];
+        adv[i][e] += red[((2 * i + 1) * 16 + e) * 64 + lane];
+      }
+    const int mykey = kw0 + 32 * kg + (lane & 31);
+    store_transposed<bf16_t, D / 32>(dk + kb, kv.ts, mykey, kv.n, 0, adk, scale, lane);
+    store_transposed<bf16_t, D / 32>(dv + kb, kv.ts, mykey, kv.n, 0, adv, 1.f, lane);
   }
 }
 
@@ -1653,7 +1774,7 @@ int check_attn(const vd_attn_desc* d) {
 //   kD4: the deferred-check forward with 4 waves, two workgroups per CU (the SIMD partners
 //          then come from different workgroups and share no barrier)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
-               kCfgLast = kD4 };
+               kPair = 8, kCfgLast = kPair };
 
 int cfg_from_env() {
   const char* e = getenv("VDIFF_ATTN_CFG");
@@ -1666,6 +1787,7 @@ int cfg_from_env() {
   if (!strcmp(e, "d8")) return (int)kD8;
   if (!strcmp(e, "d8n")) return (int)kD8N;
   if (!strcmp(e, "d4")) return (int)kD4;
+  if (!strcmp(e, "pair")) return (int)kPair;
   return -1;
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
@@ -1678,12 +1800,14 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //   D = 64 : fwd W8 17.2 ms, dQ P8 21.6 ms, dK/dV P8 29.1 ms (N = 262144); fwd D8N
   //            (deferred check, static priority) 17.7 vs W8 17.9-18.1 on the same box
   //   D = 128: fwd NB2 2.0 ms, dQ W8 2.8 ms (P4 3.7), dK/dV base 4.7 ms (N = 65536); fwd D8N
-  //            2.01 vs NB2 2.32-2.35 ms on the same box (tools/attn_ab.sh)
+  //            2.01 vs NB2 2.32-2.35 ms on the same box (tools/attn_ab.sh); dK/dV PAIR
+  //            (round 2) 3.84-3.96 vs base 4.84-4.85 ms on the same box (tools/ab_d128.sh)
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
-                    ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)))
+                    ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
+      !(env == kPair && (D != 128 || kind != 2)))  // the paired kernel: D = 128 dK/dV only
     c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
-  else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kBase);
+  else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kPair);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
   if (c == kP8 && D != 64) c = kP4;
@@ -1968,6 +2092,24 @@ int dkdv_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const 
   return vd::check_launch("attn_bwd_dkdv");
 }
 
+template <int D>
+int dkdv_pair_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k,
+                     const void* v, const void* dout, const float* nlse2, const float* ndelta,
+                     void* dk, void* dv, hipStream_t st) {
+  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+  const size_t lds = (size_t)8 * 32 * D * 2 + tile_loop_lds<bf16_t, D, true, 2>();
+  auto kern = attn_bwd_dkdv_pair_kernel<D>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(kv.n, 128), (unsigned)d->nseq);
+  kern<<<grid, 512, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                               (const bf16_t*)dout, nlse2, ndelta, (bf16_t*)dk, (bf16_t*)dv,
+                               d->seq_len, qa, d->token_stride, oa, d->o_token_stride, d->scale,
+                               kv);
+  return vd::check_launch("attn_bwd_dkdv");
+}
+
 template <typename T, int D>
 int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
                   const void* v, const void* dout, const float* lse, void* dk, void* dv,
@@ -1986,6 +2128,8 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
       if (c == kP8) return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D <= 128)
       if (c == kP4) return dkdv_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 128)
+      if (c == kPair) return dkdv_pair_launch<D>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
   }
   const BwdWs w = bwd_ws<D>(d, kv.n, cross);
   return dkdv_launch<T, D, 1, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st,
