@@ -445,7 +445,7 @@ def main():
         sampler = DDIMSampler(LinearNoiseSchedulerV2(500, 0.00005, 0.015), steps=50)
         clip = synthetic_clip(1, args.frames, args.size, 500, device, seed=100 + rank)
         model.eval()
-        with torch.no_grad():
+        with torch.no_grad(), ops.frozen_weights():
             feats = model.encode_audio(clip.audio)
             xt = torch.randn_like(clip.x0)
             for i in range(1):
@@ -470,7 +470,7 @@ def main():
             T4, S4, k4 = 25, 256, args.c4_steps
             work4 = unet_forward_work(model, (1, 195, T4, S4, S4))
             clip4 = synthetic_clip(1, T4, S4, 500, device, seed=200 + rank)
-            with torch.no_grad():
+            with torch.no_grad(), ops.frozen_weights():
                 feats4 = model.encode_audio(clip4.audio)
                 x4 = torch.randn_like(clip4.x0)
                 t = torch.full((1,), int(sampler.timesteps[0]), dtype=torch.int64, device=device)

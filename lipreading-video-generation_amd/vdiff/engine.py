@@ -16,6 +16,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
+from . import ops
 from .ddp import GradBucketer
 
 
@@ -94,7 +95,13 @@ class Trainer:
 
 @torch.no_grad()
 def sample_ddim(model, sampler, cond, audio, shape, generator=None, callback=None):
-    """DDIM sampling (build extension of test.py:51-83): audio encoded once."""
+    """DDIM sampling (build extension of test.py:51-83): audio encoded once, packed conv
+    weights reused across steps (ops.frozen_weights)."""
+    with ops.frozen_weights():
+        return _sample_ddim(model, sampler, cond, audio, shape, generator, callback)
+
+
+def _sample_ddim(model, sampler, cond, audio, shape, generator, callback):
     model.eval()
     device = cond.device
     feats = model.encode_audio(audio) if hasattr(model, "encode_audio") else audio
@@ -113,6 +120,12 @@ def sample_ddim(model, sampler, cond, audio, shape, generator=None, callback=Non
 def sample_ddpm(model, scheduler, cond, audio, shape, n_timesteps=None, generator=None,
                 callback=None):
     """Ancestral sampling as test.py:51-83 (V2 scheduler by default there)."""
+    with ops.frozen_weights():
+        return _sample_ddpm(model, scheduler, cond, audio, shape, n_timesteps, generator,
+                            callback)
+
+
+def _sample_ddpm(model, scheduler, cond, audio, shape, n_timesteps, generator, callback):
     model.eval()
     device = cond.device
     feats = model.encode_audio(audio) if hasattr(model, "encode_audio") else audio

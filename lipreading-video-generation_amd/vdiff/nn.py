@@ -260,12 +260,44 @@ class ResBlock(TimestepBlock):
         gn1, conv1 = self.in_layers[0], self.in_layers[2]
         gn2, drop, conv2 = self.out_layers[0], self.out_layers[2], self.out_layers[3]
         h = ops.group_norm_silu(x, gn1.weight, gn1.bias, gn1.num_groups, gn1.eps)
-        emb_out = self.emb_layers(emb)
+        emb_out = emb[self] if isinstance(emb, EmbTable) else self.emb_layers(emb)
         h = ops.conv(h, conv1.weight, conv1.bias, conv1.stride, conv1.padding, chan_add=emb_out)
         p = drop.p if self.training else 0.0
         h = ops.group_norm_silu(h, gn2.weight, gn2.bias, gn2.num_groups, gn2.eps, dropout=p)
         skip = self.skip_connection(x)
         return ops.conv(h, conv2.weight, conv2.bias, conv2.stride, conv2.padding, residual=skip)
+
+
+class EmbTable:
+    """Every ResBlock's emb_layers(emb) = Linear(SiLU(emb)) (unet.py:211-217) of one forward,
+    computed as ONE GEMM: the blocks share `emb`, so SiLU runs once and the per-block
+    [Cout, 256] weights are stacked into one [sum Cout, 256] operand (one launch instead of
+    one per block, forward and backward alike; gradients reach each block's own weight and
+    bias through the stacking).  Passed down TimestepEmbedSequential in place of `emb`."""
+
+    def __init__(self, emb, blocks):
+        lins = [rb.emb_layers[1] for rb in blocks]
+        w = th.cat([lin.weight for lin in lins])
+        b = th.cat([lin.bias for lin in lins])
+        out = ops.linear(ops.silu(emb), w, b)
+        self.rows = dict(zip(map(id, blocks), out.split([lin.out_features for lin in lins],
+                                                         dim=-1)))
+        self.emb = emb
+
+    def __getitem__(self, block):
+        return self.rows[id(block)]
+
+
+def emb_table(model, emb):
+    """EmbTable over the model's ResBlocks (cached list), or `emb` itself when the blocks
+    do not all share the reference emb_layers structure."""
+    blocks = getattr(model, "_resblocks", None)
+    if blocks is None:
+        blocks = [m for m in model.modules() if isinstance(m, ResBlock)]
+        ok = all(isinstance(rb.emb_layers[0], SiLU) and isinstance(rb.emb_layers[1], nn.Linear)
+                 for rb in blocks)
+        model._resblocks = blocks = blocks if ok else []
+    return EmbTable(emb, blocks) if blocks else emb
 
 
 class QKVAttentionLegacy(nn.Module):
@@ -510,6 +542,7 @@ class UNetModel(nn.Module):
             assert y.shape == (x.shape[0],)
             emb = emb + self.label_emb(y)
         h = ops.to_cl(x.type(self.dtype))
+        emb = emb_table(self, emb)
         for module in self.input_blocks:
             h = module(h, emb, context)
             hs.append(h)

@@ -160,6 +160,8 @@ class UNetAudio(UNetModel):
             emb = emb + self.label_emb(y)
         h = ops.conv(x, w, first.bias, first.stride, first.padding)
         hs.append(h)
+        from .nn import emb_table
+        emb = emb_table(self, emb)
         for module in list(self.input_blocks)[1:]:
             h = module(h, emb, context)
             hs.append(h)

@@ -31,6 +31,7 @@ import torch
 
 import _vdiff_path  # noqa: F401
 from vdiff.engine import reinit_nonzero, sample_ddim, synthetic_clip
+from vdiff.ops import frozen_weights
 
 from linear_noise_scheduler import LinearNoiseSchedulerV2
 from noise_scheduler import DDIMSampler
@@ -124,13 +125,14 @@ def sample_images(model, scheduler, img_cond, audio_cond, n_timesteps=500, *, ou
     feats = model.encode_audio(audio_cond)  # once per clip (the reference: every step)
     xt = torch.randn(shape, generator=generator, device=dev)
     x0 = None
-    for i in reversed(range(n_timesteps)):
-        t = torch.tensor([i], dtype=torch.long, device=dev)
-        eps = model(xt, img_cond, feats, t)
-        z = torch.randn(xt.shape, generator=generator, device=dev)
-        xt, x0 = scheduler.sample_prev_timestep(xt, eps, t, z=z)
-        if (i + 1) % save_every == 0 or i == 0:
-            save_frame(x0, os.path.join(out_dir, f"x0_{i}"))
+    with frozen_weights():  # packed conv weights reused across the steps
+        for i in reversed(range(n_timesteps)):
+            t = torch.tensor([i], dtype=torch.long, device=dev)
+            eps = model(xt, img_cond, feats, t)
+            z = torch.randn(xt.shape, generator=generator, device=dev)
+            xt, x0 = scheduler.sample_prev_timestep(xt, eps, t, z=z)
+            if (i + 1) % save_every == 0 or i == 0:
+                save_frame(x0, os.path.join(out_dir, f"x0_{i}"))
     print("All images have been processed and saved.")
     return x0
 
