@@ -547,6 +547,9 @@ using NoSched = BlockSched<0, 0, 0, 0, 0>;
 template <int D, bool RC, int TR = kTile>
 constexpr int pipe_stage_bytes() { return 2 * TR * D * 2 + (RC ? 2 * TR * 4 + 256 : 0); }
 
+#ifndef VD_PIPE_UNROLL
+#define VD_PIPE_UNROLL 1
+#endif
 template <typename T, int D, bool RC, int NW, typename SCH = NoSched, int TR = kTile,
           typename SF, typename GF, typename VF>
 __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, int64_t ts_a,
@@ -586,11 +589,13 @@ __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, in
       dma_rowc(stream ? r1 : r0, rcs, tok0 + part * 64, lane);
     }
   };
-  auto blk = [&](int bi) {  // bi = -1: the last block of tile -1 (the zeroed stage NST-1)
-    const char* st = smem + ((bi >> LB) & (NST - 1)) * STAGE_BYTES;
+  auto blk_at = [&](const char* st, int bi) {
     const float* rc = reinterpret_cast<const float*>(st + 4 * TE);
     return BlockRef<T>{reinterpret_cast<const T*>(st), reinterpret_cast<const T*>(st + TE * 2),
                        rc, rc + TR, 32 * (bi & (BPT - 1)), bi};
+  };
+  auto blk = [&](int bi) {  // bi = -1: the last block of tile -1 (the zeroed stage NST-1)
+    return blk_at(smem + ((bi >> LB) & (NST - 1)) * STAGE_BYTES, bi);
   };
   // Stage NST-1 stands in for tile -1: zeroed, so G(-1) (the previous block's products at
   // t = 0) reads zero rows and adds nothing -- the loop body needs no t > 0 branch.
@@ -604,26 +609,56 @@ __device__ __forceinline__ void tile_pipe(char* smem, const T* a, const T* b, in
   for (int s = 0; s < PD; ++s) issue(s);
   // One loop copy per wave role, so each tile's body is one basic block (MFMA and VALU
   // of neighbouring steps can interleave in the schedule).
+  // One tile step.  SG >= 0: the tile's ring stage is the compile-time SG (the loop is
+  // unrolled by NST), so every LDS fragment address is a loop-invariant lane offset plus
+  // an immediate; SG < 0: the stage is computed from t.
+  auto step = [&](int t, auto late_c, auto sg_c) __attribute__((always_inline)) {
+    constexpr bool LATE = decltype(late_c)::value;
+    constexpr int SG = decltype(sg_c)::value;
+    auto bk = [&](int bi, int j) __attribute__((always_inline)) {  // j: block - b0 (-1..BPT-1)
+      if constexpr (SG >= 0) {
+        constexpr int SP = (SG + NST - 1) % NST;
+        return blk_at(smem + (j < 0 ? SP : SG) * STAGE_BYTES, bi);
+      } else {
+        return blk(bi);
+      }
+    };
+    vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
+    issue(t + PD);
+    const int b0 = BPT * t;
+    if constexpr (LATE) V(bk(b0 - 1, -1));
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      S(bk(b0 + j, j));
+      G(bk(b0 + j - 1, j - 1));
+      if (!LATE || j < BPT - 1) V(bk(b0 + j, j));
+    }
+    if constexpr (SCH::on && !LATE) {
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) SCH::emit();
+    }
+  };
   auto run = [&](auto late_c) {
     constexpr bool LATE = decltype(late_c)::value;
-    for (int t = 0; t < ntiles; ++t) {
-      vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
-      issue(t + PD);
-      const int b0 = BPT * t;
-      if constexpr (LATE) V(blk(b0 - 1));
-#pragma unroll
-      for (int j = 0; j < BPT; ++j) {
-        S(blk(b0 + j));
-        G(blk(b0 + j - 1));
-        if (!LATE || j < BPT - 1) V(blk(b0 + j));
-      }
-      if constexpr (SCH::on && !LATE) {
-#pragma unroll
-        for (int j = 0; j < BPT; ++j) SCH::emit();
+    int t = 0;
+#if VD_PIPE_UNROLL
+    if constexpr (D <= 64)  // at D = 128 the unrolled copies spill
+    // Long sequences: whole groups of NST tiles with compile-time stages.  Tiles past the
+    // end are zero-filled by the DMA range check and add nothing (dQ: zero K rows; dK/dV:
+    // zero Q / dO rows and row constants), so the tile count is rounded up to NST.
+    if (ntiles >= 4 * NST) {
+      const int nt = (ntiles + NST - 1) / NST * NST;
+      for (; t < nt; t += NST) {
+        step(t, late_c, std::integral_constant<int, 0>{});
+        step(t + 1, late_c, std::integral_constant<int, 1>{});
+        step(t + 2, late_c, std::integral_constant<int, 2>{});
+        step(t + 3, late_c, std::integral_constant<int, 3>{});
       }
     }
-    if constexpr (LATE) V(blk(BPT * ntiles - 1));
-    G(blk(BPT * ntiles - 1));
+#endif
+    for (; t < ntiles; ++t) step(t, late_c, std::integral_constant<int, -1>{});
+    if constexpr (LATE) V(blk(BPT * t - 1));
+    G(blk(BPT * t - 1));
   };
   if (late) run(std::true_type{});
   else run(std::false_type{});
@@ -1456,13 +1491,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
       for (int r = 0; r < 16; ++r)
         if (key0 + acc_row(r, hh) >= n) s[r] = -INFINITY;
   };
-  auto S = [&](f32x16& s, int bi) __attribute__((always_inline)) {
+  // st: the block's ring stage (nullptr: from bi)
+  auto S = [&](f32x16& s, int bi, const char* st = nullptr) __attribute__((always_inline)) {
     s = negm;
-    mma_rows<T, D>(s, kblk(bi), 32 * (bi & 1), qf, lane);
+    mma_rows<T, D>(s, st ? reinterpret_cast<const T*>(st) : kblk(bi), 32 * (bi & 1), qf, lane);
   };
-  auto G = [&](const XOp<T>& p, int bi) __attribute__((always_inline)) {
+  auto G = [&](const XOp<T>& p, int bi, const char* st = nullptr) __attribute__((always_inline)) {
+    const T* vb = st ? reinterpret_cast<const T*>(st) + TE : vblk(bi);
 #pragma unroll
-    for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], vblk(bi), 32 * (bi & 1), 32 * i, p, lane);
+    for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], vb, 32 * (bi & 1), 32 * i, p, lane);
   };
   // MK: the block may hold keys >= n (only the last tile's blocks can)
 #if VD_DEFER_MSUM
@@ -1551,8 +1588,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
   for (int s = 0; s < PD; ++s) issue(s);
   // The last tile runs its own copy of the body, the only one that masks keys >= n: the
   // steady-state body carries no branch besides the check at its top.
-  auto tile = [&](int t, auto late_c, auto mk) __attribute__((always_inline)) {
+  // SG >= 0: tile t's ring stage as a compile-time constant (the loop unrolled by NST:
+  // LDS fragment addresses become loop-invariant lane offsets plus immediates)
+  auto tile = [&](int t, auto late_c, auto mk, auto sg_c) __attribute__((always_inline)) {
     constexpr bool LATE = decltype(late_c)::value;
+    constexpr int SG = decltype(sg_c)::value;
+    const char* cur = SG >= 0 ? smem + SG * STAGE_BYTES : nullptr;
+    const char* prv = SG >= 0 ? smem + ((SG + NST - 1) % NST) * STAGE_BYTES : nullptr;
     vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
     issue(t + PD);
     const int b0 = 2 * t;
@@ -1596,18 +1638,29 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     Sp(sb, 1);
     Gp(pb, 1);
 #else
-    S(sa, b0);
-    G(pa, b0 - 2);
+    S(sa, b0, cur);
+    G(pa, b0 - 2, prv);
     V(sa, pa, psa, b0, mk);
-    S(sb, b0 + 1);
-    G(pb, b0 - 1);
+    S(sb, b0 + 1, cur);
+    G(pb, b0 - 1, prv);
 #endif
     if constexpr (!LATE) V(sb, pb, psb, b0 + 1, mk);
   };
   auto run = [&](auto late_c) __attribute__((always_inline)) {
     constexpr bool LATE = decltype(late_c)::value;
-    for (int t = 0; t < ntiles - 1; ++t) tile(t, late_c, std::false_type{});
-    tile(ntiles - 1, late_c, std::true_type{});
+    using Dyn = std::integral_constant<int, -1>;
+    int t = 0;
+#if VD_PIPE_UNROLL
+    if constexpr (D <= 64)  // at D = 128 the unrolled copies spill (256 VGPRs)
+    for (; t + NST <= ntiles - 1; t += NST) {
+      tile(t, late_c, std::false_type{}, std::integral_constant<int, 0>{});
+      tile(t + 1, late_c, std::false_type{}, std::integral_constant<int, 1>{});
+      tile(t + 2, late_c, std::false_type{}, std::integral_constant<int, 2>{});
+      tile(t + 3, late_c, std::false_type{}, std::integral_constant<int, 3>{});
+    }
+#endif
+    for (; t < ntiles - 1; ++t) tile(t, late_c, std::false_type{}, Dyn{});
+    tile(ntiles - 1, late_c, std::true_type{}, Dyn{});
     if constexpr (LATE) V(sb, pb, psb, 2 * ntiles - 1, std::true_type{});
     check(ntiles - 1);
     G(pa, 2 * ntiles - 2);
