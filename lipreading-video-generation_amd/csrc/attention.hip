@@ -1684,7 +1684,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
   if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m + log2f(lt)) / kLog2e;
 }
 
-template <typename T, int D, int NW>
+// NB: 32-row blocks per wave (NB = 2 with 4 waves: one wave per SIMD with the whole
+// register file; each LDS fragment read feeds two MFMAs, half the LDS bytes per FLOP).
+template <typename T, int D, int NW, int NB = 1>
 __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
     const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
@@ -1692,55 +1694,76 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int seq = blockIdx.y;
-  const int q0 = blockIdx.x * (32 * NW) + wave * 32;
+  const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq);
   const bool late = VD_BWD_STAGGER && NW == 8 && wave >= 4;
 
-  RowFrag<T, D> qf, of;
-  f32x16 il, id;
-  {
-    const int myq = q0 + (lane & 31);
-    qf.load(q + base, ts, myq, n, lane);
-    qf.scale(scale * kLog2e);
-    of.load(dout + oa(seq), ots, myq, n, lane);
+  RowFrag<T, D> qf[NB], of[NB];
+  f32x16 il[NB], id[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int myq = q0 + 32 * j + (lane & 31);
+    qf[j].load(q + base, ts, myq, n, lane);
+    qf[j].scale(scale * kLog2e);
+    of[j].load(dout + oa(seq), ots, myq, n, lane);
     const float a = myq < n ? nlse2[(int64_t)seq * n + myq] : 0.f;
     const float b = myq < n ? ndelta[(int64_t)seq * n + myq] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      il[r] = a;
-      id[r] = b;
+      il[j][r] = a;
+      id[j][r] = b;
     }
   }
-  f32x16 acc[D / 32], s{}, dp{};
+  f32x16 acc[D / 32][NB], s[NB], dp[NB];
 #pragma unroll
-  for (int i = 0; i < D / 32; ++i) acc[i] = f32x16{};
-  XOp<T> ds{};
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
+#pragma unroll
+  for (int j = 0; j < NB; ++j) s[j] = dp[j] = f32x16{};  // a staggered wave's V(-1) reads them
+  // zero operands (explicitly: G of block -1 multiplies them by the zeroed ring stage, and
+  // uninitialised registers could hold NaN bit patterns)
+  XOp<T> ds[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) ds[j] = XOp<T>(f32x16{});
   // static priority for the second-dispatched half (MI355X_MICROARCH.md): 23.3 vs 23.45 ms
   // at N = 262144 (dK/dV measured no gain, so it stays off there)
   if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
-  tile_pipe<T, D, false, NW, typename std::conditional<kSchedOn, DqSched<D>, NoSched>::type,
+  tile_pipe<T, D, false, NW, typename std::conditional<kSchedOn && NB == 1, DqSched<D>, NoSched>::type,
             pipe_tr<D, NW>()>(
       smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
       [&](const BlockRef<T>& bs) {
-        s = il;
-        dp = id;
-        mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
-        mma_rows<T, D>(dp, bs.b, bs.row0, of, lane);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          s[j] = il[j];
+          dp[j] = id[j];
+        }
+        mma_rows_nb<T, D, NB>(s, bs.a, bs.row0, qf, lane);
+        mma_rows_nb<T, D, NB>(dp, bs.b, bs.row0, of, lane);
       },
       [&](const BlockRef<T>& bg) {  // dQ^T += K^T dS^T (keys past n: zero K rows)
 #pragma unroll
-        for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(acc[i], bg.a, bg.row0, 32 * i, ds, lane);
+        for (int i = 0; i < D / 32; ++i) mma_tr_nb<T, D, NB>(acc[i], bg.a, bg.row0, 32 * i, ds, lane);
       },
       [&](const BlockRef<T>&) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = fast_exp2(s[r]) * dp[r];
-        ds = XOp<T>(s);
+        for (int j = 0; j < NB; ++j) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[j][r] = fast_exp2(s[j][r]) * dp[j][r];
+          ds[j] = XOp<T>(s[j]);
+        }
       });
-  store_transposed<T, D / 32>(dq + base, ts, q0 + (lane & 31), n, 0, acc, scale, lane);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    f32x16 out[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) out[i] = acc[i][j];
+    store_transposed<T, D / 32>(dq + base, ts, q0 + 32 * j + (lane & 31), n, 0, out, scale, lane);
+  }
 }
 
-template <typename T, int D, int NW>
+template <typename T, int D, int NW, int NB = 1>
 __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
     const T* __restrict__ dout, const float* __restrict__ nlse2, const float* __restrict__ ndelta,
@@ -1749,54 +1772,82 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int seq = blockIdx.y;
-  const int k0 = blockIdx.x * (32 * NW) + wave * 32;
+  const int k0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
   const int64_t base = qa(seq), obase = oa(seq);
   const bool late = VD_BWD_STAGGER && NW == 8 && wave >= 4;
 
-  RowFrag<T, D> kf, vf;
-  kf.load(k + base, ts, k0 + (lane & 31), n, lane);
-  kf.scale(scale * kLog2e);
-  vf.load(v + base, ts, k0 + (lane & 31), n, lane);
-  f32x16 adv[D / 32], adk[D / 32], s{}, dp{};
+  RowFrag<T, D> kf[NB], vf[NB];
 #pragma unroll
-  for (int i = 0; i < D / 32; ++i) adv[i] = adk[i] = f32x16{};
-  XOp<T> pp{}, ds{};
+  for (int j = 0; j < NB; ++j) {
+    kf[j].load(k + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+    kf[j].scale(scale * kLog2e);
+    vf[j].load(v + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+  }
+  f32x16 adv[D / 32][NB], adk[D / 32][NB], s[NB], dp[NB];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) adv[i][j] = adk[i][j] = f32x16{};
+#pragma unroll
+  for (int j = 0; j < NB; ++j) s[j] = dp[j] = f32x16{};  // a staggered wave's V(-1) reads them
+  XOp<T> pp[NB], ds[NB];  // zero operands for G of block -1 (see the dQ kernel)
+#pragma unroll
+  for (int j = 0; j < NB; ++j) pp[j] = ds[j] = XOp<T>(f32x16{});
 
-  tile_pipe<T, D, true, NW, typename std::conditional<kSchedOn, DkdvSched<D>, NoSched>::type,
+  tile_pipe<T, D, true, NW, typename std::conditional<kSchedOn && NB == 1, DkdvSched<D>, NoSched>::type,
             pipe_tr<D, NW>()>(
       smem, q + base, dout + obase, ts, ots, nlse2 + (int64_t)seq * n, ndelta + (int64_t)seq * n,
       n, tid, late,
       [&](const BlockRef<T>& bs) {
-        // registers 4g..4g+3 are query rows 8g + 4hh + 0..3 of the block
+        // registers 4g..4g+3 are query rows 8g + 4hh + 0..3 of the block (the same rows
+        // for every key block j: one load, the MFMA chains start from it)
+        f32x16 ls0, dl0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 ls = *reinterpret_cast<const float4*>(bs.rc + bs.row0 + 8 * g + 4 * hh);
           const float4 dl = *reinterpret_cast<const float4*>(bs.rc1 + bs.row0 + 8 * g + 4 * hh);
-          s[4 * g + 0] = ls.x; s[4 * g + 1] = ls.y; s[4 * g + 2] = ls.z; s[4 * g + 3] = ls.w;
-          dp[4 * g + 0] = dl.x; dp[4 * g + 1] = dl.y; dp[4 * g + 2] = dl.z; dp[4 * g + 3] = dl.w;
+          ls0[4 * g + 0] = ls.x; ls0[4 * g + 1] = ls.y; ls0[4 * g + 2] = ls.z; ls0[4 * g + 3] = ls.w;
+          dl0[4 * g + 0] = dl.x; dl0[4 * g + 1] = dl.y; dl0[4 * g + 2] = dl.z; dl0[4 * g + 3] = dl.w;
         }
-        mma_rows<T, D>(s, bs.a, bs.row0, kf, lane);   // S'[q][key] - lse'
-        mma_rows<T, D>(dp, bs.b, bs.row0, vf, lane);  // dP[q][key] - delta
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          s[j] = ls0;
+          dp[j] = dl0;
+        }
+        mma_rows_nb<T, D, NB>(s, bs.a, bs.row0, kf, lane);   // S'[q][key] - lse'
+        mma_rows_nb<T, D, NB>(dp, bs.b, bs.row0, vf, lane);  // dP[q][key] - delta
       },
       [&](const BlockRef<T>& bg) {
 #pragma unroll
         for (int i = 0; i < D / 32; ++i) {
-          mma_tr<T, D>(adv[i], bg.b, bg.row0, 32 * i, pp, lane);  // dV^T += dO^T P
-          mma_tr<T, D>(adk[i], bg.a, bg.row0, 32 * i, ds, lane);  // dK^T += Q^T dS
+          mma_tr_nb<T, D, NB>(adv[i], bg.b, bg.row0, 32 * i, pp, lane);  // dV^T += dO^T P
+          mma_tr_nb<T, D, NB>(adk[i], bg.a, bg.row0, 32 * i, ds, lane);  // dK^T += Q^T dS
         }
       },
       [&](const BlockRef<T>&) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          s[r] = fast_exp2(s[r]);
-          dp[r] *= s[r];
+        for (int j = 0; j < NB; ++j) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            s[j][r] = fast_exp2(s[j][r]);
+            dp[j][r] *= s[j][r];
+          }
+          pp[j] = XOp<T>(s[j]);
+          ds[j] = XOp<T>(dp[j]);
         }
-        pp = XOp<T>(s);
-        ds = XOp<T>(dp);
       });
-  const int mykey = k0 + (lane & 31);
-  store_transposed<T, D / 32>(dk + base, ts, mykey, n, 0, adk, scale, lane);
-  store_transposed<T, D / 32>(dv + base, ts, mykey, n, 0, adv, 1.f, lane);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int mykey = k0 + 32 * j + (lane & 31);
+    f32x16 ok[D / 32], ov[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) {
+      ok[i] = adk[i][j];
+      ov[i] = adv[i][j];
+    }
+    store_transposed<T, D / 32>(dk + base, ts, mykey, n, 0, ok, scale, lane);
+    store_transposed<T, D / 32>(dv + base, ts, mykey, n, 0, ov, 1.f, lane);
+  }
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1826,8 +1877,10 @@ int check_attn(const vd_attn_desc* d) {
 //          with / without the staggered second half; other kernels keep their default
 //   kD4: the deferred-check forward with 4 waves, two workgroups per CU (the SIMD partners
 //          then come from different workgroups and share no barrier)
+//   kP4N2: the pipelined backward kernels with 4 waves x 2 blocks (one wave per SIMD,
+//          each LDS fragment feeds two MFMAs; bf16, D = 64; fwd keeps its default)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
-               kPair = 8, kCfgLast = kPair };
+               kPair = 8, kP4N2 = 9, kCfgLast = kP4N2 };
 
 int cfg_from_env() {
   const char* e = getenv("VDIFF_ATTN_CFG");
@@ -1841,6 +1894,7 @@ int cfg_from_env() {
   if (!strcmp(e, "d8n")) return (int)kD8N;
   if (!strcmp(e, "d4")) return (int)kD4;
   if (!strcmp(e, "pair")) return (int)kPair;
+  if (!strcmp(e, "p4n2")) return (int)kP4N2;
   return -1;
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
@@ -1857,7 +1911,8 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //            (round 2) 3.84-3.96 vs base 4.84-4.85 ms on the same box (tools/ab_d128.sh)
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
-      !(env == kPair && (D != 128 || kind != 2)))  // the paired kernel: D = 128 dK/dV only
+      !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
+      !(env == kP4N2 && (D != 64 || kind == 0)))     // 2-block pipelined: D = 64 backward
     c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
   else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kPair);
@@ -2047,17 +2102,17 @@ int dq_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k, co
   return vd::check_launch("attn_bwd_dq");
 }
 
-template <typename T, int D, int NW>
+template <typename T, int D, int NW, int NB = 1>
 int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                    const void* dout, const float* nlse2, const float* ndelta, void* dq,
                    hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const size_t lds = tile_pipe_lds<D, false, pipe_tr<D, NW>()>();
-  auto kern = attn_bwd_dq_pipe_kernel<T, D, NW>;
+  auto kern = attn_bwd_dq_pipe_kernel<T, D, NW, NB>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW), (unsigned)d->nseq);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq);
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
                                    ndelta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
                                    d->o_token_stride, d->scale);
@@ -2086,6 +2141,8 @@ int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, con
       if (c == kW8) return dq_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kP8) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D == 64)
+      if (c == kP4N2) return dq_pipe_launch<T, D, 4, 2>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D <= 128)
       if (c == kP4) return dq_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
   }
@@ -2128,17 +2185,17 @@ int dkdv_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k, 
   return vd::check_launch("attn_bwd_dkdv");
 }
 
-template <typename T, int D, int NW>
+template <typename T, int D, int NW, int NB = 1>
 int dkdv_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                      const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
                      hipStream_t st) {
   const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
   const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
   const size_t lds = tile_pipe_lds<D, true, pipe_tr<D, NW>()>();
-  auto kern = attn_bwd_dkdv_pipe_kernel<T, D, NW>;
+  auto kern = attn_bwd_dkdv_pipe_kernel<T, D, NW, NB>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW), (unsigned)d->nseq);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NB * NW), (unsigned)d->nseq);
   kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout, nlse2,
                                    ndelta, (T*)dk, (T*)dv, d->seq_len, qa, d->token_stride, oa,
                                    d->o_token_stride, d->scale);
@@ -2179,6 +2236,9 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
       if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kP8) return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 64)
+      if (c == kP4N2)
+        return dkdv_pipe_launch<T, D, 4, 2>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D <= 128)
       if (c == kP4) return dkdv_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 128)

@@ -65,7 +65,7 @@ def test_scores_with_large_logits():
     assert rel_l2(out, ref) < 2e-5
 
 
-CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair"]
+CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair", "p4n2"]
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
@@ -78,6 +78,17 @@ def test_bf16_kernel_shapes(cfg, C):
     with ops.attention_config(cfg):
         _check(2, C, 1, 3, 67, "joint", True, torch.bfloat16, 60 + C)
         _check(1, C, 1, 1, 21, "joint", True, torch.bfloat16, 61 + C)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+@pytest.mark.parametrize("C", [64, 128])
+def test_bf16_long_ragged_ring(cfg, C):
+    """A sequence long enough for the stage-unrolled ring loops (>= 16 tiles) whose tile
+    count is not a multiple of the 4 ring stages (N = 1157: 19 tiles, the last partial), so
+    the padded tail tiles (zero rows) and the remainder loop both run, fwd and bwd."""
+    from vdiff import ops
+    with ops.attention_config(cfg):
+        _check(1, C, 1, 1, 1157, "joint", True, torch.bfloat16, 70 + C)
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
