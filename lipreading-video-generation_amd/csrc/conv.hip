@@ -1236,6 +1236,176 @@ void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, c
                                     ca, (const bf16_t*)res);
 }
 
+// ----------------------------------------------------------------- 1x1 convs: streaming GEMM
+// A 1x1, stride-1, unpadded conv (qkv / proj_out / skip, fwd and bwd-data) is an HBM-bound
+// GEMM over pixels: Y[p][n] = sum_k X[p][k] W[n][k] with K = 32 KS <= 256 and a weight slice
+// of whole 64-channel chunks that fits the LDS.  Persistent workgroups load their weight slice (NS output channels) into LDS
+// once and stream 16-pixel tiles: each wave takes whole tiles, loads the tile's X rows
+// straight into MFMA B operands (lane = pixel, 16 B of channels each: no LDS for X), keeps
+// the next tile's loads in flight while it computes, and emits C^T = W X^T so every lane
+// stores 16 consecutive channels (two 16-B stores) of one pixel per 64-channel chunk.  Bias, per-batch channel add and the
+// residual are fused into the store.  W rows are padded by 16 B: the 16 rows of an A-operand
+// read land in distinct bank quads for every K.
+constexpr int kPwMaxLds = 40 * 1024;
+
+template <int KS>
+__global__ __launch_bounds__(256) void pw_gemm_kernel(
+    const bf16_t* __restrict__ src, int sCs, const bf16_t* __restrict__ wt, int N, int NS,
+    bf16_t* __restrict__ dst, int dNs, const float* __restrict__ bias,
+    const float* __restrict__ chan_add, int64_t ppb, const bf16_t* __restrict__ residual,
+    int64_t M) {
+  constexpr int K = 32 * KS, RS = K + 8;  // LDS row stride in bf16 (16-B pad)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* wl = reinterpret_cast<bf16_t*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbase = blockIdx.y * NS;
+  const int nsl = N - nbase < NS ? N - nbase : NS;  // channels of this slice (multiple of 16)
+  const int nrow = (nsl + 63) / 64 * 64;  // rows read by the MFMAs (zero past nsl)
+  for (int c = tid; c < nrow * (K / 8); c += 256) {
+    const int r = c / (K / 8), k8 = c % (K / 8);
+    *reinterpret_cast<uint4*>(wl + r * RS + k8 * 8) =
+        r < nsl ? *reinterpret_cast<const uint4*>(wt + (int64_t)(nbase + r) * K + k8 * 8)
+                : make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int64_t ntiles = (M + 15) / 16;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  auto load = [&](bf16x8 (&x)[KS], int64_t tile) __attribute__((always_inline)) {
+    const int64_t p = tile * 16 + fr;
+    const bool ok = tile < ntiles && p < M;
+    const bf16_t* row = src + (ok ? p : 0) * (int64_t)sCs + 8 * fq;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const uint4 v = ok ? *reinterpret_cast<const uint4*>(row + 32 * kk) : make_uint4(0, 0, 0, 0);
+      x[kk] = __builtin_bit_cast(bf16x8, v);
+    }
+  };
+  bf16x8 xc[KS], xn[KS];
+  int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  load(xc, tile);
+  for (; tile < ntiles; tile += stride) {
+    load(xn, tile + stride);  // next tile in flight while this one computes and stores
+    const int64_t p = tile * 16 + fr;
+    const bool pok = p < M;
+    const int b = chan_add ? (int)((pok ? p : 0) / ppb) : 0;
+    bf16_t* out = dst + (pok ? p : 0) * (int64_t)dNs + nbase;
+    const bf16_t* res = residual ? residual + (pok ? p : 0) * (int64_t)dNs + nbase : nullptr;
+    for (int n0 = 0; n0 < nsl; n0 += 64) {
+      // block j's A row r is channel n0 + 16 (r >> 2) + 4 j + (r & 3), so accumulator
+      // register i of block j on lane (fq, pixel) is channel n0 + 16 fq + 4 j + i: each lane
+      // ends with 16 consecutive channels of its pixel (two 16-B stores)
+      f32x4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16_t* wr = wl + (n0 + 16 * (fr >> 2) + 4 * j + (fr & 3)) * RS + 8 * fq;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(wr + 32 * kk);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xc[kk], acc[j], 0, 0, 0);
+        }
+      }
+      const int nl = n0 + 16 * fq;  // this lane's first channel within the slice
+      if (nl < nsl && pok) {
+        float o[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[4 * j + i] = acc[j][i];
+        if (bias) {
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + nbase + nl + 4 * q4);
+            o[4 * q4] += bv.x; o[4 * q4 + 1] += bv.y; o[4 * q4 + 2] += bv.z; o[4 * q4 + 3] += bv.w;
+          }
+        }
+        if (chan_add) {
+          const float* cr = chan_add + (int64_t)b * N + nbase + nl;
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * q4);
+            o[4 * q4] += cv.x; o[4 * q4 + 1] += cv.y; o[4 * q4 + 2] += cv.z; o[4 * q4 + 3] += cv.w;
+          }
+        }
+        if (res) {
+          float rv[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            load8(res + nl + 8 * h, rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[8 * h + e] += rv[e];
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v8[e] = o[8 * h + e];
+          store8(out + nl + 8 * h, v8);
+        }
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) xc[kk] = xn[kk];
+  }
+}
+
+// 1x1 conv on the streaming kernel when the shape allows (else -1): K = 32..256 in steps of
+// 32, N a multiple of 16, 16-B aligned rows, 8-B aligned output / residual rows.
+int pw_gemm_launch(const GemmGeom& g, const void* src, const void* wt, void* dst,
+                   const float* bias, const float* ca, const void* res, hipStream_t st) {
+  const int K = g.sC;
+  if (g.kt * g.kh * g.kw != 1 || g.st != 1 || g.sh != 1 || g.sw != 1 || g.pt || g.ph || g.pw)
+    return -1;
+  if (K % 32 || K > 256 || g.N % 16 || g.sCs % 8 || g.dNs % 8 || g.K != K) return -1;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(wt) & 15) ||
+      (reinterpret_cast<uintptr_t>(dst) & 15) || (reinterpret_cast<uintptr_t>(res) & 15))
+    return -1;
+  if (bias && (reinterpret_cast<uintptr_t>(bias) & 15)) return -1;
+  if (ca && ((reinterpret_cast<uintptr_t>(ca) & 15) || g.N % 4)) return -1;
+  const int row_bytes = (K + 8) * 2;
+  int NS = (kPwMaxLds / row_bytes) / 64 * 64;  // slices of whole 64-channel chunks
+  if (NS < 64) return -1;
+  int slices = (int)vd_cdiv(g.N, NS);
+  NS = (int)vd_cdiv(vd_cdiv(g.N, slices), 64) * 64;  // even slices
+  slices = (int)vd_cdiv(g.N, NS);
+  const size_t lds = (size_t)NS * row_bytes;
+  const int64_t tiles = vd_cdiv(g.M, 16);
+  int64_t wgs = vd_cdiv(tiles, 4);
+  const int64_t cap = (int64_t)256 * 8 / slices;  // persistent: <= 8 workgroups per CU in all
+  if (wgs > cap) wgs = cap < 256 ? 256 : cap;
+  const int64_t ppb = (int64_t)g.dT * g.dH * g.dW;
+  dim3 grid((unsigned)wgs, (unsigned)slices);
+#define VD_PW_CASE(KS_)                                                                          \
+  case KS_: {                                                                                    \
+    auto kern = pw_gemm_kernel<KS_>;                                                             \
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                              (int)lds);                                                         \
+    kern<<<grid, 256, lds, st>>>((const bf16_t*)src, g.sCs, (const bf16_t*)wt, g.N, NS,          \
+                                 (bf16_t*)dst, g.dNs, bias, ca, ppb, (const bf16_t*)res, g.M);   \
+    return VD_OK;                                                                                \
+  }
+  switch (K / 32) {
+    VD_PW_CASE(1) VD_PW_CASE(2) VD_PW_CASE(3) VD_PW_CASE(4)
+    VD_PW_CASE(5) VD_PW_CASE(6) VD_PW_CASE(7) VD_PW_CASE(8)
+  }
+#undef VD_PW_CASE
+  return -1;
+}
+
+#ifndef VD_PW_DEFAULT
+#define VD_PW_DEFAULT 1
+#endif
+// VDIFF_CONV_PW=0 turns the streaming 1x1 kernel off (A/B)
+const bool g_conv_pw = [] {
+  const char* e = getenv("VDIFF_CONV_PW");
+  return e ? atoi(e) != 0 : VD_PW_DEFAULT != 0;
+}();
+
 // Single-K-step GEMMs (1x1 convs with Ci <= 64: qkv, proj_out, skip) are load -> MFMA ->
 // store with nothing to overlap inside a workgroup, so the tile is picked for workgroups
 // per CU: 64 x 64 (32 KB LDS, five per CU) moves 64->192 x 262144 in 95 us against 114 us
@@ -1305,6 +1475,8 @@ template <typename T, bool TR>
 int launch_gemm(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
                 const float* ca, const void* res, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
+    if (!g_legacy_conv && g_conv_pw && pw_gemm_launch(g, src, wt, dst, bias, ca, res, st) == VD_OK)
+      return VD_OK;
     const bool unit = g.st == 1 && g.sh == 1 && g.sw == 1;
     // LDS-DMA ring: 32-bit buffer offsets, taps <= 32 (validity bits), unit-stride gather
     // when transposed

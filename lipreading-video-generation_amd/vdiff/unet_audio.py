@@ -31,6 +31,34 @@ from . import ops
 from .nn import Conv2d, Linear, UNetModel
 
 
+class _WeightNormReduce(nn.Module):
+    """w = g * v / ||v|| (norm over every dim but `dim`): the weight-norm parametrization of
+    wav2vec2's positional conv (transformers Wav2Vec2PositionalConvEmbedding, dim = 2) as a
+    plain reduction.  torch._weight_norm's last-dim kernel took 0.47 ms per call forward and
+    0.47 ms backward on MI355X for the [768, 48, 128] weight (profiles/r02_train_kernel_stats_
+    prepair.md); same math, same parameters (original0 = g, original1 = v)."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+
+    def forward(self, weight_g, weight_v):
+        dims = [d for d in range(weight_v.dim()) if d != self.dim]
+        norm = weight_v.float().pow(2).sum(dim=dims, keepdim=True).sqrt()
+        return (weight_v * (weight_g / norm)).to(weight_v.dtype)
+
+
+def _swap_weight_norm(model):
+    from torch.nn.utils.parametrizations import _WeightNorm
+    for mod in model.modules():
+        plist = getattr(getattr(mod, "parametrizations", None), "weight", None)
+        if plist is None:
+            continue
+        for i, p in enumerate(plist):
+            if isinstance(p, _WeightNorm):
+                plist[i] = _WeightNormReduce(p.dim)
+
+
 class Wav2Vec2Encoder(nn.Module):
     """unet_audio.py:10-18.  `pretrained=None` loads local weights if the HF cache has
     them (no network in this build) and otherwise builds wav2vec2-base from its config
@@ -51,6 +79,7 @@ class Wav2Vec2Encoder(nn.Module):
                               f"({type(e).__name__}); using a random-init wav2vec2-base")
         if model is None:
             model = Wav2Vec2Model(Wav2Vec2Config())
+        _swap_weight_norm(model)
         self.wav2vec2 = model
 
     def forward(self, audio_input):

@@ -26,6 +26,9 @@ CASES = [
     ((1, 128, 3, 10, 10), 128, 3, (1, 2, 2), 1),  # strided: transposed gather with stride 2
     ((2, 64, 3, 4, 32), 64, 3, 1, 1),          # bf16 kw-strip wgrad: 2 rows / step, t and b carry
     ((1, 64, 2, 3, 64), 128, 3, 1, 1),         # kw-strip wgrad: one 64-pixel row / step
+    ((1, 96, 2, 5, 7), 48, 1, 1, 0),           # streaming 1x1: K = 96 (odd K step count)
+    ((1, 256, 2, 6, 6), 768, 1, 1, 0),         # streaming 1x1: weight in 12 LDS slices
+    ((1, 64, 1, 3, 7), 40, 1, 1, 0),           # 1x1 with N % 16 != 0: igemm fallback
 ]
 
 
@@ -87,6 +90,33 @@ def test_conv_fused_epilogue(dtype):
     dl[4] = ops.to_cl(dl[4])
     dl = [t.requires_grad_(True) for t in dl]
     y = ops.conv(dl[0], dl[1], dl[2], padding=1, chan_add=dl[3], residual=dl[4])
+    y.backward(ops.to_cl(g.to(dev, dtype)))
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    assert rel_l2(y, yr) < tol
+    for a, r in zip(dl, leaves):
+        assert rel_l2(a.grad, r.grad) < 2 * tol + 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv1x1_fused_epilogue(dtype):
+    """The streaming 1x1 kernel's fused store: bias + chan_add[b, co] + residual, over a
+    ragged pixel count (B = 2, 5 x 7 x 3 = 105 pixels per batch, not a multiple of 16)."""
+    from vdiff import ops
+    x = seeded((2, 64, 3, 5, 7), 11)
+    w, b = _weights(64, 192, 1, 3, 12)
+    ca = seeded((2, 192), 14)
+    res = seeded((2, 192, 3, 5, 7), 15)
+    if dtype == torch.bfloat16:
+        x, w, res = x.bfloat16().float(), w.bfloat16().float(), res.bfloat16().float()
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b, ca, res)]
+    yr = onn.conv(leaves[0], leaves[1], leaves[2]) + leaves[3][:, :, None, None, None] + leaves[4]
+    g = seeded(yr.shape, 16)
+    yr.backward(g)
+    dl = [x.to(dev, dtype), w.to(dev), b.to(dev), ca.to(dev), res.to(dev, dtype)]
+    dl[0] = ops.to_cl(dl[0])
+    dl[4] = ops.to_cl(dl[4])
+    dl = [t.requires_grad_(True) for t in dl]
+    y = ops.conv(dl[0], dl[1], dl[2], chan_add=dl[3], residual=dl[4])
     y.backward(ops.to_cl(g.to(dev, dtype)))
     tol = 2e-6 if dtype == torch.float32 else 1e-2
     assert rel_l2(y, yr) < tol

@@ -1,5 +1,7 @@
-"""Time the single-K-step 1x1 conv forwards of the UNet3D at 128x128x16 (qkv 64->192 and
-proj 64->64 over 262144 pixels) with HIP events; VDIFF_CONV_1X1 selects the tile variant."""
+"""Time the UNet3D 1x1 convs (fwd and bwd-data) at the 128x128x16 shapes with HIP events:
+level 0 (262144 pixels: qkv 64->192, proj 64->64, skip 128->64) and level 1 (65536 pixels:
+qkv 128->384, proj 128->128).  VDIFF_CONV_PW=0 turns the streaming 1x1 kernel off
+(igemm tiles); GB/s counts the algorithmic bytes (X in + Y out, bf16)."""
 import os
 import sys
 
@@ -8,24 +10,37 @@ sys.path.insert(0, os.path.join(ROOT, "lipreading-video-generation_amd"))
 
 import torch  # noqa: E402
 
-from vdiff import ops  # noqa: E402
+from vdiff import _lib, ops  # noqa: E402
 
-for Ci, Co, P in ((64, 192, 262144), (64, 64, 262144), (32, 96, 262144)):
-    x = ops.to_cl(torch.randn(1, Ci, P, device="cuda", dtype=torch.bfloat16))
-    w = torch.randn(Co, Ci, 1, device="cuda") / Ci ** 0.5
-    b = torch.randn(Co, device="cuda")
-    y = ops.conv(x, w, b)
-    ref = (torch.einsum("oc,cp->op", w[:, :, 0], x[0].float()) + b[:, None])
-    err = float((y[0].float() - ref).norm() / ref.norm())
+
+def timeit(fn, reps=20):
     for _ in range(3):
-        ops.conv(x, w, b)
+        fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(20):
-        ops.conv(x, w, b)
+    for _ in range(reps):
+        fn()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 20
+    return e0.elapsed_time(e1) / reps
+
+
+tag = "pw" if os.environ.get("VDIFF_CONV_PW", "1") != "0" else "igemm"
+for Ci, Co, P in ((64, 192, 262144), (64, 64, 262144), (128, 64, 262144), (128, 384, 65536),
+                  (128, 128, 65536)):
+    x = ops.to_cl(torch.randn(1, Ci, P, device="cuda", dtype=torch.bfloat16))
+    w = torch.nn.Parameter(torch.randn(Co, Ci, 1, device="cuda") / Ci ** 0.5, requires_grad=False)
+    b = torch.randn(Co, device="cuda")
+    dy = ops.to_cl(torch.randn(1, Co, P, device="cuda", dtype=torch.bfloat16))
+    xg = x.detach().requires_grad_(True)
+    with ops.frozen_weights():  # packed weights cached: time the conv kernels alone
+        y = ops.conv(x, w, b)
+        ref = (torch.einsum("oc,cp->op", w[:, :, 0], x[0].float()) + b[:, None])
+        err = float((y[0].float() - ref).norm() / ref.norm())
+        ms_f = timeit(lambda: ops.conv(x, w, b))
+        # fwd + bwd-data (x only needs a gradient: no weight / bias gradient kernels)
+        ms_b = timeit(lambda: torch.autograd.grad(ops.conv(xg, w, b), xg, dy)) - ms_f
     gb = (P * Ci + P * Co) * 2 / 1e9
-    print(f"variant {os.environ.get('VDIFF_CONV_1X1', '0')} {Ci:4d}->{Co:4d} x {P}: {ms * 1e3:7.1f} us "
-          f"(incl. weight pack) {gb / ms * 1e3:6.0f} GB/s  rel-L2 {err:.1e}", flush=True)
+    print(f"{tag:6s} {Ci:4d}->{Co:4d} x {P}: fwd {ms_f * 1e3:7.1f} us {gb / ms_f * 1e3:6.0f} GB/s"
+          f"  bwd-data {ms_b * 1e3:7.1f} us {gb / ms_b * 1e3:6.0f} GB/s  rel-L2 {err:.1e}",
+          flush=True)
