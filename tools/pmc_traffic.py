@@ -21,13 +21,14 @@ CALIB_ELEMS = 1 << 27
 CALIB_READ = 2 * CALIB_ELEMS * 2
 CALIB_WRITE = CALIB_ELEMS * 2
 
-_ATTN = re.compile(r"(attn_\w+?)_kernel<[^,<>]+,\s*(\d+)")
+_ATTN = re.compile(r"(attn_\w+?)_kernel<(?:[^,<>]+,\s*)?(\d+)")
+_VARIANT = re.compile(r"_(pipe|defer|pair)$")  # kernel variants share the launch's key
 
 
 def kernel_key(name: str) -> str:
     m = _ATTN.search(name)
     if m:
-        return f"{m.group(1)}_d{m.group(2)}"
+        return f"{_VARIANT.sub('', m.group(1))}_d{m.group(2)}"
     if "QSample" in name:
         return "calib_q_sample"
     base = re.sub(r"^void\s+", "", name).split("(")[0]
