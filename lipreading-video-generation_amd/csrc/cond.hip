@@ -72,6 +72,37 @@ __global__ void cond_concat_kernel(const T* __restrict__ image, const T* __restr
   }
 }
 
+// One thread per (pixel, 16-byte chunk of output channels): the pixel's coordinates are
+// decoded once per chunk (32-bit), the chunk's channels gathered from their section, and
+// the chunk written with one 16-B store.  Needs out_cstride % (16 / sizeof(T)) == 0.
+// (The per-element form above took 233 us for 262144 pixels x 200 channels: four 64-bit
+// divisions per element.)
+template <typename T>
+__global__ void cond_concat_vec_kernel(const T* __restrict__ image, const T* __restrict__ imc,
+                                       const T* __restrict__ audio, T* __restrict__ out, int P,
+                                       int T_, int H, int W, int Cx, int h, int w, int Ci, int Ca,
+                                       int Cs) {
+  constexpr int E = 16 / sizeof(T);
+  const int nch = Cs / E;
+  const int64_t n = (int64_t)P * nch;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i / nch), c0 = (int)(i - (int64_t)p * nch) * E;
+    const int x = p % W, r = p / W, y = r % H, bt = r / H, b = bt / T_;
+    const int ys = nearest_src(y, h, H), xs = nearest_src(x, w, W);
+    const T* ip = image + (int64_t)p * Cx;
+    const T* cp = imc + ((int64_t)(b * h + ys) * w + xs) * Ci - Cx;
+    const T* ap = audio + (int64_t)bt * Ca - Cx - Ci;
+    T v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int c = c0 + e;
+      v[e] = c < Cx ? ip[c] : c < Cx + Ci ? cp[c] : c < Cx + Ci + Ca ? ap[c] : T{};
+    }
+    *reinterpret_cast<uint4*>(out + (int64_t)p * Cs + c0) = *reinterpret_cast<const uint4*>(v);
+  }
+}
+
 // d_audio[b][t][c] = sum over (y, x); grid (B*T, chunks of rows), atomics across chunks
 template <typename T>
 __global__ void cond_audio_bwd_kernel(const T* __restrict__ dout, float* __restrict__ da, int H,
@@ -137,6 +168,17 @@ int vd_cond_concat(const void* image, const void* imc, const void* audio, void* 
   VD_REQUIRE(B > 0 && T > 0 && H > 0 && W > 0 && Cx > 0 && h > 0 && w > 0, "bad shape");
   VD_REQUIRE(out_cstride >= Cx + Ci + Ca, "out_cstride %d < %d", out_cstride, Cx + Ci + Ca);
   const int64_t n = (int64_t)B * T * H * W * out_cstride;
+  const int64_t P = (int64_t)B * T * H * W;
+  const int E = dtype == VD_BF16 ? 8 : 4;
+  if (out_cstride % E == 0 && P < (1ll << 31) && (reinterpret_cast<uintptr_t>(out) & 15) == 0)
+    return VD_DISPATCH_DTYPE(dtype, Tp, {
+      const int64_t work = P * (out_cstride / E);
+      int64_t g = vd_cdiv(work, kBlock);
+      if (g > 65536) g = 65536;
+      cond_concat_vec_kernel<Tp><<<(unsigned)g, kBlock, 0, VD_STREAM(stream)>>>(
+          (const Tp*)image, (const Tp*)imc, (const Tp*)audio, (Tp*)out, (int)P, T, H, W, Cx, h,
+          w, Ci, Ca, out_cstride);
+    });
   return VD_DISPATCH_DTYPE(dtype, Tp, {
     cond_concat_kernel<Tp><<<grid_for(n), kBlock, 0, VD_STREAM(stream)>>>(
         (const Tp*)image, (const Tp*)imc, (const Tp*)audio, (Tp*)out, B, T, H, W, Cx, h, w, Ci,

@@ -152,3 +152,30 @@ def test_conv_pack_weight(transpose):
         ref = torch.zeros(Co, taps, Cip)
         ref[:, :, :Ci] = wr.permute(0, 2, 1)
     assert torch.equal(got.cpu(), ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("five,cpad", [(True, 200), (True, 0), (False, 72)])
+def test_cond_concat_matches_torch(dtype, five, cpad):
+    """vd_cond_concat (unet_audio.py:52-61): [image | nearest-resized image-cond | audio |
+    zero pad], bit-exact against the torch composition (a pure gather).  cpad 200 / 72: the
+    16-B chunk kernel; cpad 0 (195 channels): the per-element kernel."""
+    import torch.nn.functional as F
+    from vdiff import ops
+    B, T, H, W, Cx, Ci, Ca, h, w = 2, 3, 12, 10, 3, 64, 128, 5, 7
+    g = torch.Generator().manual_seed(5)
+    img = torch.randn((B, Cx, T, H, W) if five else (B, Cx, H, W), generator=g).to(dtype)
+    imc = torch.randn(B, Ci, h, w, generator=g).to(dtype)
+    aud = torch.randn(B, T if five else 1, Ca, generator=g).to(dtype)
+    ic = F.interpolate(imc.float(), size=(H, W), mode="nearest").to(dtype)
+    if five:
+        ic = ic[:, :, None].expand(B, Ci, T, H, W)
+        au = aud.permute(0, 2, 1)[:, :, :, None, None].expand(B, Ca, T, H, W)
+    else:
+        au = aud[:, 0, :, None, None].expand(B, Ca, H, W)
+    ref = torch.cat([img, ic, au], 1)
+    cs = max(cpad, ref.shape[1])
+    if cs > ref.shape[1]:
+        ref = F.pad(ref, [0, 0] * (ref.dim() - 2) + [0, cs - ref.shape[1]])
+    out = ops.cond_concat(img.to(dev), imc.to(dev), aud.to(dev), cpad=cpad)
+    assert torch.equal(out.cpu(), ref)
