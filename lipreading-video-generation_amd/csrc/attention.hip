@@ -1160,6 +1160,143 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_kernel(
   }
 }
 
+// ------------------------------------------------------------------ dK / dV, head_dim 256
+// Role-split pairs: waves w and w + 4 (one SIMD) own the same 32 keys.  Wave A (w < 4) keeps
+// K in registers and the full-width dV^T accumulators; wave B keeps V and dK^T.  Per 32-query
+// block A computes S' and P = exp2(S' - lse') and hands P (fp32) to B through LDS; B computes
+// dP - delta, dS = P * (dP - delta) and dK^T += Q^T dS while A runs dV^T += dO^T P.  Each
+// product runs once: 8 N^2 D executed against 12 for the output-column split, and each wave
+// needs 64 + 128 + ~40 registers (the full-width single-wave form needs > 512).
+//   A: [S MFMAs, exp] bar2 [write P] bar1 [dV MFMAs]
+//   B: [dP MFMAs]     bar2           bar1 [read P, dS, dK MFMAs]
+// bar2 orders A's write of block h after B's read of block h - 1; bar1 B's read after A's
+// write.  Both roles run their own copy of the tile loop (their accumulators never share a
+// live range) and pass the same barriers in the same order.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt untouched
+  __builtin_amdgcn_s_barrier();
+}
+
+// VD_ROLE_NW: waves per workgroup (8: two per SIMD, 256 registers each; 4: one per SIMD)
+#ifndef VD_ROLE_NW
+#define VD_ROLE_NW 4
+#endif
+// VD_ROLE_G: k-steps per scheduling-fenced group in the role kernel's products (16: none)
+#ifndef VD_ROLE_G
+#define VD_ROLE_G 16
+#endif
+constexpr int kRoleG = VD_ROLE_G;
+// mma_rows / mma_tr in groups of G k-steps / tiles behind scheduling fences: bounds how far
+// the compiler hoists LDS operand reads (registers, at 256 per wave)
+template <int D, int G>
+__device__ __forceinline__ void mma_rows_fenced(f32x16& acc, const bf16_t* tile, int row0,
+                                                const RowFrag<bf16_t, D>& b, int lane) {
+  const int r = row0 + (lane & 31), hh = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (s % G == 0) __builtin_amdgcn_sched_barrier(0);
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + toff<bf16_t, D>(r, 16 * s + 8 * hh));
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b.f[s], acc, 0, 0, 0);
+  }
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_role_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ nlse2,
+    const float* __restrict__ ndelta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int n,
+    SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale, KvAddr kv, FwdSplit qsplit) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NP = NW / 2;  // wave pairs: wave w (A) and w + NP (B)
+  const int hh = lane >> 5, pair = wave % NP;
+  const int seq = blockIdx.y, qz = blockIdx.z;
+  const int qofs = qz * qsplit.tps * kTile;
+  const int nq = qsplit.part ? min(n - qofs, qsplit.tps * kTile) : n;
+  const int k0 = blockIdx.x * (32 * NP) + pair * 32;
+  const int mykey = k0 + (lane & 31);
+  const int64_t base = qa(seq) + (int64_t)qofs * ts, obase = oa(seq) + (int64_t)qofs * ots;
+  const int64_t kb = kv.a(seq);
+  const float* rc0 = nlse2 + (int64_t)seq * n + qofs;
+  const float* rc1 = ndelta + (int64_t)seq * n + qofs;
+  // P hand-off of this pair: [4 register groups][64 lanes][4 floats] (conflict-free b128)
+  constexpr int RING = nstage<D>() * (2 * kTile * D * 2 + 768);  // tile_loop_lds<bf16, D, RC>
+  float* xch = reinterpret_cast<float*>(smem + RING) + pair * 1024;
+  float* part = qsplit.part ? qsplit.part + ((int64_t)qz * gridDim.y + seq) * kv.n * (2 * D)
+                            : nullptr;
+  // registers 4g..4g+3 are query rows 8g + 4hh + 0..3 of the block
+  auto rows = [&](f32x16& x, const float* L) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 c = *reinterpret_cast<const float4*>(L + 8 * g + 4 * hh);
+      x[4 * g + 0] = c.x; x[4 * g + 1] = c.y; x[4 * g + 2] = c.z; x[4 * g + 3] = c.w;
+    }
+  };
+  if (wave < NP) {  // A: S, P, dV
+    RowFrag<bf16_t, D> kf;
+    kf.load(k + kb, kv.ts, mykey, kv.n, lane);
+    kf.scale(scale * kLog2e);
+    f32x16 adv[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) adv[i] = f32x16{};
+    tile_loop<bf16_t, D, true, NW>(smem, q + base, dout + obase, ts, ots, rc0, rc1, nq, tid,
+                                   [&](int, const bf16_t* Qt, const bf16_t* Ot, const float* L) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x16 sx;
+        rows(sx, L + 32 * h);
+        mma_rows_fenced<D, kRoleG>(sx, Qt, 32 * h, kf, lane);  // S'[q][key] - lse'
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sx[r] = fast_exp2(sx[r]);
+        const XOp<bf16_t> pp(sx);
+        lds_barrier();  // bar2
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(xch + (g * 64 + lane) * 4) =
+              make_float4(sx[4 * g], sx[4 * g + 1], sx[4 * g + 2], sx[4 * g + 3]);
+        lds_barrier();  // bar1
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i) {
+          if (kRoleG < 16 && i % 2 == 0) __builtin_amdgcn_sched_barrier(0);
+          mma_tr<bf16_t, D>(adv[i], Ot, 32 * h, 32 * i, pp, lane);
+        }
+      }
+    });
+    if (part) store_transposed<float, D / 32>(part + D, 2 * D, mykey, kv.n, 0, adv, 1.f, lane);
+    else store_transposed<bf16_t, D / 32>(dv + kb, kv.ts, mykey, kv.n, 0, adv, 1.f, lane);
+  } else {  // B: dP, dS, dK
+    RowFrag<bf16_t, D> vf;
+    vf.load(v + kb, kv.ts, mykey, kv.n, lane);
+    f32x16 adk[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) adk[i] = f32x16{};
+    tile_loop<bf16_t, D, true, NW>(smem, q + base, dout + obase, ts, ots, rc0, rc1, nq, tid,
+                                   [&](int, const bf16_t* Qt, const bf16_t* Ot, const float* L) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x16 dp;
+        rows(dp, L + 64 + 32 * h);
+        mma_rows_fenced<D, kRoleG>(dp, Ot, 32 * h, vf, lane);  // dP[q][key] - delta
+        lds_barrier();  // bar2
+        lds_barrier();  // bar1
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 pv = *reinterpret_cast<const float4*>(xch + (g * 64 + lane) * 4);
+          dp[4 * g + 0] *= pv.x; dp[4 * g + 1] *= pv.y; dp[4 * g + 2] *= pv.z; dp[4 * g + 3] *= pv.w;
+        }
+        const XOp<bf16_t> ds(dp);
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i) {
+          if (kRoleG < 16 && i % 2 == 0) __builtin_amdgcn_sched_barrier(0);
+          mma_tr<bf16_t, D>(adk[i], Qt, 32 * h, 32 * i, ds, lane);
+        }
+      }
+    });
+    if (part) store_transposed<float, D / 32>(part, 2 * D, mykey, kv.n, 0, adk, scale, lane);
+    else store_transposed<bf16_t, D / 32>(dk + kb, kv.ts, mykey, kv.n, 0, adk, scale, lane);
+  }
+}
+
 // dK | dV = sum over the query splits of the fp32 partials [split][nseq][nkv][dK D | dV D]
 // (one thread per 8 columns)
 template <typename T, int D>
@@ -1877,10 +2014,11 @@ int check_attn(const vd_attn_desc* d) {
 //          with / without the staggered second half; other kernels keep their default
 //   kD4: the deferred-check forward with 4 waves, two workgroups per CU (the SIMD partners
 //          then come from different workgroups and share no barrier)
+//   kRole: head_dim-256 dK/dV with role-split wave pairs (attn_bwd_dkdv_role_kernel)
 //   kP4N2: the pipelined backward kernels with 4 waves x 2 blocks (one wave per SIMD,
 //          each LDS fragment feeds two MFMAs; bf16, D = 64; fwd keeps its default)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
-               kPair = 8, kP4N2 = 9, kCfgLast = kP4N2 };
+               kPair = 8, kP4N2 = 9, kRole = 10, kCfgLast = kRole };
 
 int cfg_from_env() {
   const char* e = getenv("VDIFF_ATTN_CFG");
@@ -1895,6 +2033,7 @@ int cfg_from_env() {
   if (!strcmp(e, "d4")) return (int)kD4;
   if (!strcmp(e, "pair")) return (int)kPair;
   if (!strcmp(e, "p4n2")) return (int)kP4N2;
+  if (!strcmp(e, "role")) return (int)kRole;
   return -1;
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
@@ -1912,10 +2051,12 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
-      !(env == kP4N2 && (D != 64 || kind == 0)))     // 2-block pipelined: D = 64 backward
+      !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
+      !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
   else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kPair);
+  else if (D == 256 && kind == 2) c = kRole;
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
   if (c == kP8 && D != 64) c = kP4;
@@ -1957,6 +2098,17 @@ int q_splits(const vd_attn_desc* d, int nkv) {
   return s;
 }
 
+// query splits of the role-split head_dim-256 dK/dV grid (16 NW keys per workgroup)
+int role_q_splits(const vd_attn_desc* d, int nkv) {
+  const int64_t wgs = vd_cdiv(nkv, 16 * VD_ROLE_NW) * d->nseq;
+  if (wgs >= 256) return 1;
+  int s = (int)((256 + wgs - 1) / wgs);
+  if (s > 16) s = 16;
+  const int64_t tiles = vd_cdiv(d->seq_len, kTile);
+  while (s > 1 && tiles / s < 4) --s;
+  return s;
+}
+
 // Backward workspace: [ndelta rows][nlse2 rows][64 floats][dQ KV-split partials]
 // [dK/dV query-split partials]; rows = nseq * seq_len (queries).
 struct BwdWs {
@@ -1970,6 +2122,8 @@ BwdWs bwd_ws(const vd_attn_desc* d, int nkv, bool cross) {
   if (d->dtype == VD_BF16 && (cross || pick_cfg(D, true, 1) == kBase))
     w.sdq = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv);
   if (cross || (d->dtype == VD_BF16 && pick_cfg(D, true, 2) == kBase)) w.sq = q_splits<D>(d, nkv);
+  else if (D == 256 && d->dtype == VD_BF16 && pick_cfg(D, true, 2) == kRole)
+    w.sq = role_q_splits(d, nkv);
   w.dq_off = 2 * rows + 64;
   w.kv_off = w.dq_off + (w.sdq > 1 ? (size_t)w.sdq * rows * D : 0);
   const size_t kvp = w.sq > 1 ? (size_t)w.sq * d->nseq * nkv * 2 * D : 0;
@@ -2220,6 +2374,36 @@ int dkdv_pair_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void
   return vd::check_launch("attn_bwd_dkdv");
 }
 
+template <int D, int NW = VD_ROLE_NW>
+int dkdv_role_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k,
+                     const void* v, const void* dout, const float* nlse2, const float* ndelta,
+                     void* dk, void* dv, hipStream_t st, float* part, int sq) {
+  const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+  const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+  const size_t lds = tile_loop_lds<bf16_t, D, true>() + (NW / 2) * 1024 * sizeof(float);
+  auto kern = attn_bwd_dkdv_role_kernel<D, NW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  if (!part) sq = 1;
+  FwdSplit qsplit{sq > 1 ? part : nullptr, split_tps(d->seq_len, sq)};
+  if (sq > 1) sq = (int)vd_cdiv(vd_cdiv(d->seq_len, kTile), qsplit.tps);
+  dim3 grid((unsigned)vd_cdiv(kv.n, 16 * NW), (unsigned)d->nseq, (unsigned)sq);
+  kern<<<grid, 64 * NW, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                               (const bf16_t*)dout, nlse2, ndelta, (bf16_t*)dk, (bf16_t*)dv,
+                               d->seq_len, qa, d->token_stride, oa, d->o_token_stride, d->scale,
+                               kv, qsplit);
+  if (sq > 1) {
+    const int rc = vd::check_launch("attn_bwd_dkdv");
+    if (rc) return rc;
+    const int64_t work = (int64_t)d->nseq * kv.n * (2 * D / 8);
+    int g = (int)vd_cdiv(work, 256);
+    if (g > 4096) g = 4096;
+    attn_dkdv_sum_kernel<bf16_t, D><<<g, 256, 0, st>>>(qsplit.part, sq, d->nseq, kv.n,
+                                                       (bf16_t*)dk, (bf16_t*)dv, kv.a, kv.ts);
+  }
+  return vd::check_launch("attn_bwd_dkdv");
+}
+
 template <typename T, int D>
 int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
                   const void* v, const void* dout, const float* lse, void* dk, void* dv,
@@ -2243,6 +2427,12 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
       if (c == kP4) return dkdv_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 128)
       if (c == kPair) return dkdv_pair_launch<D>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 256)
+      if (c == kRole) {
+        const BwdWs w = bwd_ws<D>(d, kv.n, cross);
+        return dkdv_role_launch<D>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st,
+                                   reinterpret_cast<float*>(ws) + w.kv_off, w.sq);
+      }
   }
   const BwdWs w = bwd_ws<D>(d, kv.n, cross);
   return dkdv_launch<T, D, 1, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st,

@@ -65,7 +65,7 @@ def test_scores_with_large_logits():
     assert rel_l2(out, ref) < 2e-5
 
 
-CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair", "p4n2"]
+CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair", "p4n2", "role"]
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
@@ -81,7 +81,7 @@ def test_bf16_kernel_shapes(cfg, C):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("C", [64, 128, 256])
 def test_bf16_long_ragged_ring(cfg, C):
     """A sequence long enough for the stage-unrolled ring loops (>= 16 tiles) whose tile
     count is not a multiple of the 4 ring stages (N = 1157: 19 tiles, the last partial), so
@@ -127,7 +127,7 @@ def test_bf16_lagged_max_rescale_default_shapes(C):
 
 def test_config_hook_rejects_unknown():
     from vdiff import _lib, ops
-    assert _lib.lib().vd_attention_set_config(10) == -2
+    assert _lib.lib().vd_attention_set_config(11) == -2
     with pytest.raises(ValueError):
         ops.attention_config("fast")
 
