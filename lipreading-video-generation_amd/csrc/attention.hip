@@ -1194,7 +1194,7 @@ __device__ __forceinline__ void mma_rows_fenced(f32x16& acc, const bf16_t* tile,
   const int r = row0 + (lane & 31), hh = lane >> 5;
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    if (s % G == 0) __builtin_amdgcn_sched_barrier(0);
+    if (G < D / 16 && s % G == 0) __builtin_amdgcn_sched_barrier(0);
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + toff<bf16_t, D>(r, 16 * s + 8 * hh));
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b.f[s], acc, 0, 0, 0);
   }
