@@ -24,6 +24,7 @@ import os
 
 import warnings
 
+import torch
 import torch as th
 import torch.nn as nn
 
@@ -46,6 +47,53 @@ class _WeightNormReduce(nn.Module):
         dims = [d for d in range(weight_v.dim()) if d != self.dim]
         norm = weight_v.float().pow(2).sum(dim=dims, keepdim=True).sqrt()
         return (weight_v * (weight_g / norm)).to(weight_v.dtype)
+
+
+def _mask_hidden_states(self, hidden_states, mask_time_indices=None, attention_mask=None):
+    """transformers Wav2Vec2Model._mask_hidden_states (SpecAugment in training) with the
+    same masks (the same numpy draws of _compute_mask_indices) applied by torch.where
+    instead of a boolean index_put: the index_put's nonzero and the pageable mask upload made
+    the host wait for the GPU at every train step (measured 6.6 ms of idle GPU per step in
+    the wav2vec2 forward); the mask now goes up asynchronously from pinned memory."""
+    from transformers.models.wav2vec2.modeling_wav2vec2 import _compute_mask_indices
+    cfg = self.config
+    if not getattr(cfg, "apply_spec_augment", True):
+        return hidden_states
+    B, L, Hd = hidden_states.size()
+    dev = hidden_states.device
+
+    def upload(m):
+        t = torch.from_numpy(m) if not torch.is_tensor(m) else m
+        if t.device.type == "cpu" and dev.type == "cuda":
+            t = t.pin_memory().to(dev, non_blocking=True)
+        return t.to(device=dev, dtype=torch.bool)
+
+    if mask_time_indices is not None:
+        mt = upload(mask_time_indices)
+    elif cfg.mask_time_prob > 0 and self.training:
+        mt = upload(_compute_mask_indices((B, L), mask_prob=cfg.mask_time_prob,
+                                          mask_length=cfg.mask_time_length,
+                                          attention_mask=attention_mask,
+                                          min_masks=cfg.mask_time_min_masks))
+    else:
+        mt = None
+    if mt is not None:
+        hidden_states = torch.where(mt[..., None], self.masked_spec_embed.to(hidden_states.dtype),
+                                    hidden_states)
+    if cfg.mask_feature_prob > 0 and self.training:
+        mf = upload(_compute_mask_indices((B, Hd), mask_prob=cfg.mask_feature_prob,
+                                          mask_length=cfg.mask_feature_length,
+                                          min_masks=cfg.mask_feature_min_masks))
+        hidden_states = torch.where(mf[:, None, :], hidden_states.new_zeros(()), hidden_states)
+    return hidden_states
+
+
+def _patch_wav2vec2(model):
+    """Host-overhead fixes that keep the math: weight norm as a reduction, SpecAugment
+    masks without host syncs."""
+    import types
+    _swap_weight_norm(model)
+    model._mask_hidden_states = types.MethodType(_mask_hidden_states, model)
 
 
 def _swap_weight_norm(model):
@@ -79,7 +127,7 @@ class Wav2Vec2Encoder(nn.Module):
                               f"({type(e).__name__}); using a random-init wav2vec2-base")
         if model is None:
             model = Wav2Vec2Model(Wav2Vec2Config())
-        _swap_weight_norm(model)
+        _patch_wav2vec2(model)
         self.wav2vec2 = model
 
     def forward(self, audio_input):
