@@ -4,8 +4,8 @@
 # rocprofv3 --kernel-trace --stats of the very same bench.py invocation.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-bash tools/pmc_attn.sh --only 64 > gpurun_out/pmc_run.log 2>&1 || { tail -20 gpurun_out/pmc_run.log; exit 1; }
-cp gpurun_out/pmc/pmc_traffic.json profiles/pmc_traffic.json
+[ -n "$NO_PMC" ] || bash tools/pmc_attn.sh --only 64 > gpurun_out/pmc_run.log 2>&1 || { tail -20 gpurun_out/pmc_run.log; exit 1; }
+[ -n "$NO_PMC" ] || cp gpurun_out/pmc/pmc_traffic.json profiles/pmc_traffic.json
 timeout -k 10 900 python -u bench.py > gpurun_out/r02_bench.json 2> gpurun_out/r02_bench.err || { tail -20 gpurun_out/r02_bench.err; exit 1; }
 tail -c 600 gpurun_out/r02_bench.json
 rm -rf /tmp/prof_r02
