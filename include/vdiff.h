@@ -50,6 +50,11 @@ int vd_device_info(char* buf, int buflen);
  * t: int64[B]; out: fp32[B, dim]. */
 int vd_timestep_embedding(const int64_t* t, int B, int dim, float max_period,
                           float* out, void* stream);
+/* Same, with the frequency table f[dim/2] (fp32, device) supplied by the caller -- the
+ * reference computes it on the host (utils.py:150-152: torch CPU exp), so a caller that
+ * builds it the same way gets the reference's bit-identical arguments t_b * f_i. */
+int vd_timestep_embedding_tab(const int64_t* t, int B, int dim, const float* freqs,
+                              float* out, void* stream);
 
 /* ---- DDPM / DDIM scheduler math ----------------------------------------
  * Tables are fp32 device arrays of length num_timesteps; t is int64[B];

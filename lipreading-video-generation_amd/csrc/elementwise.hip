@@ -18,8 +18,9 @@ inline int grid_for(int64_t work) {
 }
 
 // ------------------------------------------------------------ timestep embedding
+// freqs: the caller's table (nullptr: computed here)
 __global__ void temb_kernel(const int64_t* __restrict__ t, int B, int dim, float log_max_period,
-                            float* __restrict__ out) {
+                            const float* __restrict__ freqs, float* __restrict__ out) {
   const int half = dim / 2;
   const int n = B * dim;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -28,7 +29,7 @@ __global__ void temb_kernel(const int64_t* __restrict__ t, int B, int dim, float
     if (j < 2 * half) {
       const int f = j < half ? j : j - half;
       // utils.py:150-152: exp(-ln(max_period) * arange(half) / half) in fp32
-      const float freq = expf(-log_max_period * (float)f / (float)half);
+      const float freq = freqs ? freqs[f] : expf(-log_max_period * (float)f / (float)half);
       const float arg = (float)t[b] * freq;
       v = j < half ? cosf(arg) : sinf(arg);
     }
@@ -348,8 +349,17 @@ int vd_timestep_embedding(const int64_t* t, int B, int dim, float max_period, fl
   VD_REQUIRE(t && out, "null argument");
   VD_REQUIRE(B > 0 && dim > 0, "bad shape B=%d dim=%d", B, dim);
   temb_kernel<<<grid_for((int64_t)B * dim), kBlock, 0, VD_STREAM(stream)>>>(
-      t, B, dim, logf(max_period), out);
+      t, B, dim, logf(max_period), nullptr, out);
   return vd::check_launch("vd_timestep_embedding");
+}
+
+int vd_timestep_embedding_tab(const int64_t* t, int B, int dim, const float* freqs, float* out,
+                              void* stream) {
+  VD_REQUIRE(t && out && (freqs || dim < 2), "null argument");
+  VD_REQUIRE(B > 0 && dim > 0, "bad shape B=%d dim=%d", B, dim);
+  temb_kernel<<<grid_for((int64_t)B * dim), kBlock, 0, VD_STREAM(stream)>>>(t, B, dim, 0.f,
+                                                                            freqs, out);
+  return vd::check_launch("vd_timestep_embedding_tab");
 }
 
 int vd_q_sample(const void* x0, const void* eps, void* xt, const int64_t* t, const float* sqrt_acp,

@@ -50,6 +50,7 @@ _SIGS = {
     "vd_last_error": (C.c_char_p, []),
     "vd_device_info": (_i, [C.c_char_p, _i]),
     "vd_timestep_embedding": (_i, [_vp, _i, _i, _f, _vp, _vp]),
+    "vd_timestep_embedding_tab": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "vd_q_sample": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i, _vp]),
     "vd_p_sample_v1": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i, _vp]),
     "vd_p_sample_v2": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i,

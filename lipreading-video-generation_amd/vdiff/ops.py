@@ -85,9 +85,29 @@ def timestep_embedding(timesteps: torch.Tensor, dim: int, max_period: float = 10
         t = t.to(torch.int64)
     t = t.contiguous()
     out = torch.empty(t.numel(), dim, dtype=torch.float32, device=t.device)
-    _lib.call("vd_timestep_embedding", _p(t), t.numel(), dim, float(max_period), _p(out),
-              _stream(t))
+    if dim < 2:
+        _lib.call("vd_timestep_embedding", _p(t), t.numel(), dim, float(max_period), _p(out),
+                  _stream(t))
+        return out
+    _lib.call("vd_timestep_embedding_tab", _p(t), t.numel(), dim,
+              _p(_temb_freqs(dim, max_period, t.device)), _p(out), _stream(t))
     return out
+
+
+_TEMB_FREQS = {}
+
+
+def _temb_freqs(dim, max_period, device):
+    """utils.py:150-152 exactly as the reference evaluates it (torch CPU fp32), uploaded once
+    per (dim, max_period, device): the kernel then multiplies the same fp32 frequencies."""
+    key = (dim, float(max_period), str(device))
+    f = _TEMB_FREQS.get(key)
+    if f is None:
+        half = dim // 2
+        f = torch.exp(-math.log(max_period) * torch.arange(start=0, end=half, dtype=torch.float32)
+                      / half).to(device)
+        _TEMB_FREQS[key] = f
+    return f
 
 
 def _flat(x: torch.Tensor) -> torch.Tensor:

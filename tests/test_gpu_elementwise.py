@@ -22,9 +22,14 @@ def test_timestep_embedding_golden():
     g = golden("schedulers.npz")
     for dim in (64, 65, 128):
         out = ops.timestep_embedding(g["temb_t"].to(dev), dim).cpu()
-        # cos/sin(t * f) with t <= 499: one ulp of the fp32 frequency (GPU expf vs the
-        # host exp the reference uses) moves the angle by up to ~3e-5
-        torch.testing.assert_close(out, g[f"temb_{dim}"], atol=1e-4, rtol=0)
+        # the frequency table is the reference's own host computation (torch CPU fp32 exp),
+        # but torch's vectorised CPU exp is not correctly rounded and its result depends on
+        # the host's SIMD path: one frequency per table differs by 1 ulp between this build
+        # container and the GPU box, which moves cos/sin(t f) at t <= 499 by up to 1.5e-5
+        # (measured).  The other entries agree to a few ulps of values in [-1, 1].
+        ref = g[f"temb_{dim}"]
+        torch.testing.assert_close(out, ref, atol=3e-5, rtol=0)
+        assert ((out - ref).abs() > 1e-6).float().mean() < 0.03
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
