@@ -1118,25 +1118,39 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_dma_kernel(
   const rsrc_t rs_a = make_rsrc(src, (uint32_t)((int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2));
   const rsrc_t rs_b = make_rsrc(wt, (uint32_t)((int64_t)g.N * g.K * 2));
 
+  // K-step cursor: issue() is called for s = 0, 1, 2, ... in order, so the step's (tap,
+  // channel step) and the tap's (a, b, c) advance incrementally -- the divisions by the
+  // runtime csteps / kh*kw / kw took ~100 scalar instructions per step (the CU's scalar
+  // unit, shared by all its waves, was close to saturated)
+  int cur_ci = 0, cur_tap = 0, cur_a = 0, cur_b = 0, cur_c = 0, cur_toff = 0;
   auto issue = [&](int s) {  // K step s into ring stage s % NST
     char* st = smem + (s % NST) * STAGE;
-    const bool live = s < nk;
-    const int tap = live ? s / csteps : 0;
-    const int c0 = live ? (s - tap * csteps) * kIgBK : 0;
-    const int ta = tap / khw, rem = tap - ta * khw;
-    const int tb = rem / g.kw, tc = rem - tb * g.kw;
-    const int toff = ((ta * g.sH + tb) * g.sW + tc) * g.sCs * 2;
+    const bool live = s < nk;  // steps past the end: every piece out of range (zero fill)
+    const int tap = live ? cur_tap : 0, c0 = cur_ci * kIgBK, toff = cur_toff;
+    if (++cur_ci == csteps) {  // next tap: its (a, b, c) and source offset, once per tap
+      cur_ci = 0;
+      ++cur_tap;
+      if (++cur_c == g.kw) {
+        cur_c = 0;
+        if (++cur_b == g.kh) {
+          cur_b = 0;
+          ++cur_a;
+        }
+      }
+      cur_toff = ((cur_a * g.sH + cur_b) * g.sW + cur_c) * g.sCs * 2;
+    }
     const int astep = (TR ? -toff : toff) + c0 * 2;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
-      const bool ok = live && c0 + a_c[i] < C && ((a_ok[i] >> tap) & 1u);
+      // bitwise, not short-circuit: && here compiled to exec-mask branches per piece
+      const bool ok = live & (c0 + a_c[i] < C) & (((a_ok[i] >> tap) & 1u) != 0);
       dma_lds<16>(rs_a, lds_addr(st + (wave * IA + i) * 1024),
                   ok ? (uint32_t)(a_off[i] + astep) : 0x80000000u);
     }
     const int bstep = (tap * C + c0) * 2;
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
-      const bool ok = live && c0 + b_c[i] < C;
+      const bool ok = live & (c0 + b_c[i] < C);
       dma_lds<16>(rs_b, lds_addr(st + A_BYTES + (wave * IB + i) * 1024),
                   ok ? (uint32_t)(b_off[i] + bstep) : 0x80000000u);
     }
@@ -1442,7 +1456,17 @@ int launch_igemm_dma(const GemmGeom& g, const void* src, const void* wt, void* d
   // three-stage ring on every UNet shape (tools/conv_ab4.sh).  N that is a multiple of 64 but
   // not of 128 (the qkv conv, N = 192) takes 64-wide tiles: no half-empty column tile.
   if (g.N <= 64 || (g.N % 128 != 0 && g.N % 64 == 0)) {
-    launch_igd<256, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+    // 128 x 64 tiles (three workgroups per CU): since the K-step cursor made the DMA issue
+    // cheap, they beat 256 x 64 (the 200-channel first conv 455 -> 382 us, 64->64 at
+    // 262144 pixels 111 -> 109 us; profiles/r02_ab_conv_scalar.txt).  VDIFF_CONV_N64 (A/B):
+    // 0 = 256 x 64, 2 = 64 x 64
+    static const int n64 = [] {
+      const char* e = getenv("VDIFF_CONV_N64");
+      return e ? atoi(e) : 1;
+    }();
+    if (n64 == 0) launch_igd<256, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+    else if (n64 == 2) launch_igd<64, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
+    else launch_igd<128, 64, 4, TR, 2>(g, src, wt, dst, bias, ca, res, st);
   } else if (vd_cdiv(g.M, 128) * vd_cdiv(g.N, 128) < 512) {
     // fewer than two 128 x 128 tiles per CU: 64 x 128 (256->256 at 16x32x32: 1.00 -> 0.91 ms)
     launch_igd<64, 128, 2, TR, 2>(g, src, wt, dst, bias, ca, res, st);
