@@ -1930,6 +1930,9 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   XOp<T> pp[NB], ds[NB];  // zero operands for G of block -1 (see the dQ kernel)
 #pragma unroll
   for (int j = 0; j < NB; ++j) pp[j] = ds[j] = XOp<T>(f32x16{});
+#ifdef VD_DKDV_PRIO
+  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);  // A/B: as the dQ kernel
+#endif
 
   tile_pipe<T, D, true, NW, typename std::conditional<kSchedOn && NB == 1, DkdvSched<D>, NoSched>::type,
             pipe_tr<D, NW>()>(

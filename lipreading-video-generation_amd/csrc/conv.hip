@@ -914,10 +914,11 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
   auto issue = [&](int s) {
     char* st = smem + (s % NST) * STAGE;
     const bool live = s < nsteps;
-    const int64_t ms = mbeg + (int64_t)s * 64;
+    // 32-bit offsets: the launcher takes this kernel only when dY and X span < 2 GiB
+    const int ms = (int)mbeg + s * 64, me = (int)mend;
 #pragma unroll
     for (int i = 0; i < PY; ++i) {
-      const bool ok = live && ms + y_p[i] < mend && y_col[i] < g.Co;
+      const bool ok = live & (ms + y_p[i] < me) & (y_col[i] < g.Co);
       dma_lds<16>(rs_y, lds_addr(st + (wave * PY + i) * 1024),
                   ok ? (uint32_t)(((ms + y_p[i]) * g.yCs + y_col[i]) * 2) : 0x80000000u);
     }
@@ -925,9 +926,9 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
     for (int i = 0; i < PX; ++i) {
       uint32_t off = 0x80000000u;
       if (ONE) {
-        if (live && ms + x_j[i] < mend && x_col[i] < g.Ci)
+        if (live & (ms + x_j[i] < me) & (x_col[i] < g.Ci))
           off = (uint32_t)(((ms + x_j[i]) * g.xCs + x_col[i]) * 2);
-      } else if (live && x_rr[i] >= 0 && x_col[i] < g.Ci) {
+      } else if (live & (x_rr[i] >= 0) & (x_col[i] < g.Ci)) {
         int b = cb, t = ct, h = chh + x_rr[i];
         while (h >= g.Ho) {
           h -= g.Ho;
@@ -939,7 +940,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
         const int ti = t - g.pt + ta, hi = h - g.ph + tb, wi = cw + x_j[i] - g.pw;
         if (b < g.B && (unsigned)ti < (unsigned)g.Ti && (unsigned)hi < (unsigned)g.Hi &&
             (unsigned)wi < (unsigned)g.Wi) {
-          const int64_t pix = (((int64_t)b * g.Ti + ti) * g.Hi + hi) * g.Wi + wi;
+          const int pix = ((b * g.Ti + ti) * g.Hi + hi) * g.Wi + wi;
           off = (uint32_t)((pix * g.xCs + x_col[i]) * 2);
         }
       }
