@@ -623,8 +623,8 @@ class ConvFn(torch.autograd.Function):
         want_ca = has_ca and ctx.needs_input_grad[3]
         if want_b or want_ca:
             sums = channel_sums(dyp)[:, :Co]  # [B, Co] fp32: one pass over dY for both
-            if want_b:
-                db = sums.sum(0).to(bdt)
+            if want_b:  # B = 1 (the bench clip): the row itself, no reduction launch
+                db = (sums[0] if B == 1 else sums.sum(0)).to(bdt)
             if want_ca:
                 dca = sums.reshape(ca_shape)
         if has_res and ctx.needs_input_grad[4]:
