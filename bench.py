@@ -63,6 +63,8 @@ def parse():
                     help="frames of the bounded CPU-baseline clip (config-2 model, "
                          "spatial_temporal)")
     ap.add_argument("--only", choices=["train", "ddim", "vivit", "all"], default="all")
+    ap.add_argument("--ddim-eager", action="store_true",
+                    help="DDIM legs without the HIP-graph replay (A/B)")
     ap.add_argument("--vivit-steps", type=int, default=20,
                     help="timed ViViT fine-tune steps (BASELINE config 5); 0 skips the leg")
     ap.add_argument("--vivit-batch", type=int, default=16, help="clips per GPU (reference: 16)")
@@ -96,6 +98,22 @@ def build_model(args, device, audio_attention=False):
                           audio_encoder_pretrained=False, audio_attention=audio_attention)
     reinit_nonzero(model, seed=1234)
     return model.to(device)
+
+
+def ddim_stepper(args, model, sampler, cond, feats, xt):
+    """One DDIM denoising step per call, i -> the update from sampler.timesteps[i]: the
+    product's HIP-graph replay (vdiff.engine.DDIMGraph, as engine.sample_ddim runs it) or,
+    with --ddim-eager, the eager UNet forward + sampler.step."""
+    from vdiff.engine import DDIMGraph
+    if not args.ddim_eager:
+        return DDIMGraph(model, sampler, cond, feats, xt).step
+    state = {"x": xt}
+
+    def step(i):
+        t = torch.full((xt.shape[0],), int(sampler.timesteps[i]), dtype=torch.int64,
+                       device=xt.device)
+        state["x"], _ = sampler.step(state["x"], model(state["x"], cond, feats, t), i)
+    return step
 
 
 def barrier_sync(world):
@@ -448,16 +466,15 @@ def main():
         with torch.no_grad(), ops.frozen_weights():
             feats = model.encode_audio(clip.audio)
             xt = torch.randn_like(clip.x0)
-            for i in range(1):
-                t = torch.full((1,), int(sampler.timesteps[i]), dtype=torch.int64, device=device)
-                xt, _ = sampler.step(xt, model(xt, clip.cond, feats, t), i)
+            step = ddim_stepper(args, model, sampler, clip.cond, feats, xt)
+            step(0)  # warm-up (and, graphed, the capture)
             barrier_sync(world)
             t0 = time.perf_counter()
             for i in range(1, 1 + kd):
-                t = torch.full((1,), int(sampler.timesteps[i]), dtype=torch.int64, device=device)
-                xt, _ = sampler.step(xt, model(xt, clip.cond, feats, t), i)
+                step(i)
             barrier_sync(world)
             el = max_over_ranks(time.perf_counter() - t0, world, device)
+            del step
         ddim = {"metric": "DDIM steps/sec (50-step DDIM, B=1 clip, replicas)",
                 "value": round(world * kd / el, 4), "unit": "steps/s",
                 "ms_per_step": round(el / kd * 1e3, 2),
@@ -473,16 +490,15 @@ def main():
             with torch.no_grad(), ops.frozen_weights():
                 feats4 = model.encode_audio(clip4.audio)
                 x4 = torch.randn_like(clip4.x0)
-                t = torch.full((1,), int(sampler.timesteps[0]), dtype=torch.int64, device=device)
-                x4, _ = sampler.step(x4, model(x4, clip4.cond, feats4, t), 0)  # warm-up step
+                step4 = ddim_stepper(args, model, sampler, clip4.cond, feats4, x4)
+                step4(0)  # warm-up step
                 barrier_sync(world)
                 t0 = time.perf_counter()
                 for i in range(1, 1 + k4):
-                    t = torch.full((1,), int(sampler.timesteps[i]), dtype=torch.int64,
-                                    device=device)
-                    x4, _ = sampler.step(x4, model(x4, clip4.cond, feats4, t), i)
+                    step4(i)
                 barrier_sync(world)
                 el4 = max_over_ranks(time.perf_counter() - t0, world, device)
+                del step4
             result["ddim_config4"] = {
                 "metric": "DDIM steps/sec, 256x256x25 UNet3D (BASELINE config 4, test.py path)",
                 "value": round(world * k4 / el4, 4), "unit": "steps/s",

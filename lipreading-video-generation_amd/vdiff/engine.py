@@ -11,6 +11,7 @@ Differences from the reference loops (all deliberate):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -101,12 +102,77 @@ def sample_ddim(model, sampler, cond, audio, shape, generator=None, callback=Non
         return _sample_ddim(model, sampler, cond, audio, shape, generator, callback)
 
 
+class DDIMGraph:
+    """One deterministic DDIM denoising step -- UNet forward + vd_ddim_step -- captured once
+    as a HIP graph and replayed per step (no per-kernel launch gaps, no host work per
+    step).  The sample lives in a static buffer updated in place; the step's timesteps are
+    copied device-to-device from the sampler's table before each replay.  Use inside
+    ops.frozen_weights() (the graph reads the cached packed conv weights); eta must be 0."""
+
+    def __init__(self, model, sampler, cond, feats, xt):
+        if sampler.eta != 0:
+            raise ValueError("DDIMGraph: eta = 0 (deterministic DDIM) only")
+        dev = xt.device
+        B = xt.shape[0]
+        self.model, self.sampler = model, sampler
+        self.cond, self.feats = cond, feats
+        self.xt = xt.clone()
+        self.t_all = sampler.timesteps.to(dev).view(-1, 1).expand(-1, B).contiguous()
+        self.tp_all = sampler.prev_timesteps.to(dev).view(-1, 1).expand(-1, B).contiguous()
+        self.t = self.t_all[0].clone()
+        self.tp = self.tp_all[0].clone()
+        self.acp = sampler._acp(dev)
+        self.graph = None
+        self.x0 = None
+
+    def _body(self):
+        eps = self.model(self.xt, self.cond, self.feats, self.t)
+        xp, x0 = ops.ddim_step(self.xt, eps.to(self.xt.dtype), self.t, self.tp, self.acp,
+                               eta=0.0, clip=self.sampler.clip_x0)
+        self.xt.copy_(xp.view_as(self.xt))
+        return x0
+
+    def _capture(self):
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream(device=self.xt.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):  # eager warm-up: packed weights, tables, workspaces
+            keep = self.xt.clone()
+            self._body()
+            self.xt.copy_(keep)
+        cur.wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.x0 = self._body()
+
+    def step(self, i):
+        """Denoise from sampler.timesteps[i]; returns (x_prev, x0) (static buffers)."""
+        self.t.copy_(self.t_all[i])
+        self.tp.copy_(self.tp_all[i])
+        if self.graph is None:
+            self._capture()
+        self.graph.replay()
+        return self.xt, self.x0.view_as(self.xt)
+
+
+def _use_graph(device, sampler):
+    return (device.type == "cuda" and sampler.eta == 0
+            and os.environ.get("VDIFF_DDIM_GRAPH", "1") != "0")
+
+
 def _sample_ddim(model, sampler, cond, audio, shape, generator, callback):
     model.eval()
     device = cond.device
     feats = model.encode_audio(audio) if hasattr(model, "encode_audio") else audio
     xt = torch.randn(shape, generator=generator, device=device)
     x0 = None
+    if _use_graph(device, sampler):
+        g = DDIMGraph(model, sampler, cond, feats, xt)
+        for i in range(sampler.steps):
+            xt, x0 = g.step(i)
+            if callback is not None:
+                callback(i, xt, x0)
+        return xt.clone(), x0.clone()
     for i in range(sampler.steps):
         t = torch.full((shape[0],), int(sampler.timesteps[i]), dtype=torch.int64, device=device)
         eps = model(xt, cond, feats, t)

@@ -472,14 +472,14 @@ def _pack_weight(weight, Co, Ci, taps, Cip, Cop, transpose, dt):
     """torch [Co][Ci][*k] weight -> packed fwd [Co][taps][Cip] / bwd [Cip][taps][Cop] operand."""
     key = None
     # parameters only: a temporary (a padded or stacked weight) may reuse a freed address
-    if (frozen_weights.depth and isinstance(weight, torch.nn.Parameter)
-            and not torch.cuda.is_current_stream_capturing()):
+    if frozen_weights.depth and isinstance(weight, torch.nn.Parameter):
         key = (weight.data_ptr(), tuple(weight.shape), weight._version, Cip, Cop, transpose, dt)
         hit = frozen_weights.cache.get(key)
-        if hit is not None:
-            return hit
+        if hit is not None:  # also while a graph is captured: the graph reads the cached
+            return hit       # operand, which outlives it inside the same context
     out = _pack_weight_now(weight, Co, Ci, taps, Cip, Cop, transpose, dt)
-    if key is not None:
+    # never insert a tensor allocated during capture (it lives in the graph's pool)
+    if key is not None and not torch.cuda.is_current_stream_capturing():
         frozen_weights.cache[key] = out
     return out
 
