@@ -1990,6 +1990,424 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   }
 }
 
+// ================================================================== fragment-pipelined backward
+// (round 2, cfg "sp", the head_dim-64 default).  The compiler schedules every LDS fragment
+// read of the kernels above right before its MFMA behind an lgkmcnt(0) (tools/kseq.py: the
+// 'R W M' pattern), so each MFMA of a wave waits a full LDS latency; with one wave per SIMD
+// (p4n2) the matrix pipe idles about as long as it works.  Here the reads of the NEXT MFMA
+// group are issued before the current group, and sched_barriers pin MFMAs and LDS reads in
+// that order while VALU / SALU / transcendental work may move across them (mask 0x406), so
+// the softmax still fills the MFMA gaps.  One wave per SIMD: 4 waves x 2 blocks of 32 rows
+// (64 keys per wave for dK/dV, 64 queries for dQ) with the whole 512-register file.
+// MFMA-group order per 64-row tile t (blocks b0 = 2t, b1 = 2t + 1):
+//   [wait + barrier] R:S(b0) M:G(b0-2) R:G(b0-1) M:S(b0) R:S(b1) M:G(b0-1) R:G(b0) M:S(b1)
+// S(b): the block's score products; G(b): its gradient products, two groups later, so the
+// softmax of block b (V(b)) has the G(b-1) and S(b+1) groups (32 MFMAs) to hide in; s / dp
+// and P / dS are kept per block parity.  R:S(b) reads tile t only, R:G(b0-1) tile t-1 (still
+// resident: the ring keeps t-1, t while t+1, t+2 land).
+#ifndef VD_SP_MASK
+#define VD_SP_MASK 0
+#endif
+#define VD_SP_FENCE() __builtin_amdgcn_sched_barrier(VD_SP_MASK)
+#ifndef VD_SP_PRIO  // A/B: static priority for the second wave half (8 waves)
+#define VD_SP_PRIO 0
+#endif
+#ifndef VD_SP_NV
+#define VD_SP_NV 3
+#endif
+#ifndef VD_SP_NVG  // dK/dV: the whole softmax of a block in one G group
+#define VD_SP_NVG 6
+#endif
+// An MFMA group region: NM x {1 MFMA, NV VALU} (the softmax half placed in the region)
+#ifndef VD_SP_IGLP
+#define VD_SP_IGLP 1
+#endif
+template <int NM, int NV>
+__device__ __forceinline__ void sp_interleave() {
+  if constexpr (!VD_SP_IGLP) return;
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+  }
+}
+
+// Row fragments of a 32-row block over D (the A operand of S = rows . frag^T)
+template <int D>
+__device__ __forceinline__ void sp_rows(bf16x8 (&f)[D / 16], const bf16_t* tile, int row0,
+                                        int lane) {
+  const int r = row0 + (lane & 31), hh = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+    f[s] = *reinterpret_cast<const bf16x8*>(tile + toff<bf16_t, D>(r, 16 * s + 8 * hh));
+}
+// accumulator-layout row constants of a 32-row block (register 4g+e = row 8g + 4hh + e)
+__device__ __forceinline__ f32x16 sp_rowc(const float* rc, int row0, int lane) {
+  const int hh = lane >> 5;
+  f32x16 x;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 v = *reinterpret_cast<const float4*>(rc + row0 + 8 * g + 4 * hh);
+    x[4 * g + 0] = v.x; x[4 * g + 1] = v.y; x[4 * g + 2] = v.z; x[4 * g + 3] = v.w;
+  }
+  return x;
+}
+
+template <int D, int NW, int NB>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_sp_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ nlse2,
+    const float* __restrict__ ndelta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int n,
+    SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
+  static_assert(D == 64 && (NB == 1 || NB == 2), "fragment pipeline: D = 64, 1-2 blocks");
+  using T = bf16_t;
+  constexpr int NST = 4, TE = kTile * D;
+  constexpr int NMG = 2 * NB * (D / 32) * 2;  // MFMAs per G group
+  constexpr int STAGE_BYTES = pipe_stage_bytes<D, true, kTile>();
+  constexpr int PER_TILE = 2 * dma_ipw<D, NW, kTile>() + 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int seq = blockIdx.y;
+  const int k0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
+  const int64_t base = qa(seq), obase = oa(seq);
+  const int ntiles = (n + kTile - 1) / kTile;
+
+  RowFrag<T, D> kf[NB], vf[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    kf[j].load(k + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+    kf[j].scale(scale * kLog2e);
+    vf[j].load(v + base, ts, k0 + 32 * j + (lane & 31), n, lane);
+  }
+  // One set of S / dP accumulators: the row constants (-lse', -delta) of block b are read
+  // straight into them (once per key block: a shared copy would cost 32 registers or 32
+  // moves) at the head of R:G(b-1), after V(b-1) consumed them.  One set of P / dS
+  // operands: G(b) reads them one group after V(b) wrote them, in the group where V(b+1)
+  // overwrites them.
+  f32x16 adv[D / 32][NB], adk[D / 32][NB], s[NB], dp[NB];
+  XOp<T> pp[NB], ds[NB];  // zero: G(-2), G(-1) add nothing
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) adv[i][j] = adk[i][j] = f32x16{};
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    pp[j] = ds[j] = XOp<T>(f32x16{});
+    dp[j] = f32x16{};  // V(-1) in the first step: p = 0, dS = 0
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[j][r] = -INFINITY;
+  }
+  bf16x8 fa[D / 16], fb[D / 16];      // R:S -- Q rows, dO rows of the block
+  bf16x8 gv[D / 32][2], gk[D / 32][2];  // R:G -- dO^T, Q^T fragments of the block
+
+  const auto ra = make_rsrc(q + base, seq_bytes(n, ts, D, 2));
+  const auto rb = make_rsrc(dout + obase, seq_bytes(n, ots, D, 2));
+  const auto r0 = make_rsrc(nlse2 + (int64_t)seq * n, (uint32_t)n * 4u);
+  const auto r1 = make_rsrc(ndelta + (int64_t)seq * n, (uint32_t)n * 4u);
+  const uint32_t tsa = (uint32_t)(ts * 2), tsb = (uint32_t)(ots * 2);
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    char* st = smem + (t & (NST - 1)) * STAGE_BYTES;
+    const int tok0 = t * kTile;
+    dma_tile<D, NW, kTile>(ra, st, tok0, n, tsa, wave, lane);
+    dma_tile<D, NW, kTile>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
+    // waves 0 / 1 stage the two row constants, waves 2 / 3 a throw-away copy (one vmcnt)
+    char* rcs = st + 4 * TE + (wave < 2 ? wave * kTile * 4 : 2 * kTile * 4);
+    dma_rowc(wave == 1 ? r1 : r0, rcs, tok0, lane);
+  };
+  auto tA = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES); };
+  auto tB = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES + TE * 2); };
+  auto tR = [&](int sg) { return reinterpret_cast<const float*>(smem + sg * STAGE_BYTES + 4 * TE); };
+  auto readS = [&](int sg, int row0) __attribute__((always_inline)) {
+    sp_rows<D>(fa, tA(sg), row0, lane);
+    sp_rows<D>(fb, tB(sg), row0, lane);
+  };
+  auto readRC = [&](int sg, int row0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      s[j] = sp_rowc(tR(sg), row0, lane);
+      dp[j] = sp_rowc(tR(sg) + kTile, row0, lane);
+    }
+  };
+  auto readG = [&](int sg, int row0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) {
+      load_tr<D>(gv[i], tB(sg), row0, 32 * i, lane);
+      load_tr<D>(gk[i], tA(sg), row0, 32 * i, lane);
+    }
+  };
+  auto mmaS = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int ss = 0; ss < D / 16; ++ss)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ss], kf[j].f[ss], s[j], 0, 0, 0);
+#pragma unroll
+    for (int ss = 0; ss < D / 16; ++ss)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ss], vf[j].f[ss], dp[j], 0, 0, 0);
+  };
+  auto mmaG = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          adv[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[i][s2], pp[j].b[s2], adv[i][j], 0, 0, 0);
+          adk[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gk[i][s2], ds[j].b[s2], adk[i][j], 0, 0, 0);
+        }
+  };
+  auto softmax = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[j][r] = fast_exp2(s[j][r]);
+        dp[j][r] *= s[j][r];
+      }
+      pp[j] = XOp<T>(s[j]);
+      ds[j] = XOp<T>(dp[j]);
+    }
+  };
+
+  {  // stage NST-1 stands in for tile -1 (zero rows: G(-1) reads it)
+    uint4* z = reinterpret_cast<uint4*>(smem + (NST - 1) * STAGE_BYTES);
+    for (int i = tid; i < STAGE_BYTES / 16; i += 64 * NW) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  if (VD_SP_PRIO && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  vm_drain();
+  issue(0);
+  issue(1);
+  readG(NST - 1, 0);  // G(-2): zero fragments of the zeroed stage
+  // tile step with a compile-time ring stage SG (the loop is unrolled by NST; tiles past the
+  // end are zero rows with zero row constants and add nothing, so the count is rounded up)
+  auto step = [&](int t, auto sg_c) __attribute__((always_inline)) {
+    constexpr int SG = decltype(sg_c)::value, SP = (SG + NST - 1) % NST;
+    vm_wait_barrier<PER_TILE>();  // tile t landed; tile t-2 no longer read
+    issue(t + 2);
+    VD_SP_FENCE();
+    readS(SG, 0);                 // R:S(b0)
+    VD_SP_FENCE();
+    mmaG();                       // M:G(b0-2) + V(b0-1)
+    softmax();
+    sp_interleave<NMG, VD_SP_NVG>();
+    VD_SP_FENCE();
+    readRC(SG, 0);                // R:G(b0-1), headed by the row constants of b0
+    readG(SP, 32);
+    VD_SP_FENCE();
+    mmaS();                       // M:S(b0)
+    VD_SP_FENCE();
+    readS(SG, 32);                // R:S(b1)
+    VD_SP_FENCE();
+    mmaG();                       // M:G(b0-1) + V(b0)
+    softmax();
+    sp_interleave<NMG, VD_SP_NVG>();
+    VD_SP_FENCE();
+    readRC(SG, 32);               // R:G(b0), headed by the row constants of b1
+    readG(SG, 0);
+    VD_SP_FENCE();
+    mmaS();                       // M:S(b1)
+    VD_SP_FENCE();
+  };
+  const int nt = (ntiles + NST - 1) / NST * NST;
+  for (int t = 0; t < nt; t += NST) {
+    step(t, std::integral_constant<int, 0>{});
+    step(t + 1, std::integral_constant<int, 1>{});
+    step(t + 2, std::integral_constant<int, 2>{});
+    step(t + 3, std::integral_constant<int, 3>{});
+  }
+  mmaG();  // G(2nt-2) (fragments already read) + V(2nt-1), then G(2nt-1)
+  softmax();
+  readG((nt - 1) & (NST - 1), 32);
+  mmaG();
+  vm_drain();
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int mykey = k0 + 32 * j + (lane & 31);
+    f32x16 ok[D / 32], ov[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) {
+      ok[i] = adk[i][j];
+      ov[i] = adv[i][j];
+    }
+    store_transposed<T, D / 32>(dk + base, ts, mykey, n, 0, ok, scale, lane);
+    store_transposed<T, D / 32>(dv + base, ts, mykey, n, 0, ov, 1.f, lane);
+  }
+}
+
+// dQ on the same fragment pipeline: 64 queries per wave (2 blocks); K / V tiles stream.
+// S(b): S^T = K Q^T and dP^T = V dO^T from K / V rows; G(b): dQ^T += K^T dS^T (K^T by
+// transposed reads of the K tile).
+template <int D, int NW, int NB>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_sp_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ nlse2,
+    const float* __restrict__ ndelta, bf16_t* __restrict__ dq, int n, SeqAddr qa, int64_t ts,
+    SeqAddr oa, int64_t ots, float scale) {
+  static_assert(D == 64 && (NB == 1 || NB == 2), "fragment pipeline: D = 64, 1-2 blocks");
+  using T = bf16_t;
+  constexpr int NST = 4, TE = kTile * D;
+  constexpr int NMS = 2 * NB * (D / 16), NMG = NB * (D / 32) * 2;  // MFMAs per S / G group
+  constexpr int STAGE_BYTES = pipe_stage_bytes<D, false, kTile>();
+  constexpr int PER_TILE = 2 * dma_ipw<D, NW, kTile>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int seq = blockIdx.y;
+  const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
+  const int64_t base = qa(seq);
+  const int ntiles = (n + kTile - 1) / kTile;
+
+  RowFrag<T, D> qf[NB], of[NB];
+  f32x16 il[NB], id[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int myq = q0 + 32 * j + (lane & 31);
+    qf[j].load(q + base, ts, myq, n, lane);
+    qf[j].scale(scale * kLog2e);
+    of[j].load(dout + oa(seq), ots, myq, n, lane);
+    const float a = myq < n ? nlse2[(int64_t)seq * n + myq] : 0.f;
+    const float b = myq < n ? ndelta[(int64_t)seq * n + myq] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      il[j][r] = a;
+      id[j][r] = b;
+    }
+  }
+  f32x16 acc[D / 32][NB], s[2][NB], dp[2][NB];
+  XOp<T> ds[2][NB];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) ds[p][j] = XOp<T>(f32x16{});
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {  // V(-1) in the first step: dS = 0
+    dp[1][j] = f32x16{};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[1][j][r] = -INFINITY;
+  }
+  bf16x8 fa[D / 16], fb[D / 16];  // R:S -- K rows, V rows of the block
+  bf16x8 gk[D / 32][2];           // R:G -- K^T fragments of the block
+
+  const auto ra = make_rsrc(k + base, seq_bytes(n, ts, D, 2));
+  const auto rb = make_rsrc(v + base, seq_bytes(n, ts, D, 2));
+  const uint32_t tsb = (uint32_t)(ts * 2);
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    char* st = smem + (t & (NST - 1)) * STAGE_BYTES;
+    dma_tile<D, NW, kTile>(ra, st, t * kTile, n, tsb, wave, lane);
+    dma_tile<D, NW, kTile>(rb, st + TE * 2, t * kTile, n, tsb, wave, lane);
+  };
+  auto tA = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES); };
+  auto tB = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES + TE * 2); };
+  auto readS = [&](int sg, int row0) __attribute__((always_inline)) {
+    sp_rows<D>(fa, tA(sg), row0, lane);
+    sp_rows<D>(fb, tB(sg), row0, lane);
+  };
+  auto readG = [&](int sg, int row0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) load_tr<D>(gk[i], tA(sg), row0, 32 * i, lane);
+  };
+  auto mmaS = [&](int par) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      s[par][j] = il[j];
+      dp[par][j] = id[j];
+    }
+#pragma unroll
+    for (int ss = 0; ss < D / 16; ++ss)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        s[par][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ss], qf[j].f[ss], s[par][j], 0, 0, 0);
+#pragma unroll
+    for (int ss = 0; ss < D / 16; ++ss)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        dp[par][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ss], of[j].f[ss], dp[par][j], 0, 0, 0);
+  };
+  auto mmaG = [&](int par) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gk[i][s2], ds[par][j].b[s2], acc[i][j], 0, 0, 0);
+  };
+  // half h of V(b): block h (NB = 2), or registers 8h..8h+7 of the one block (NB = 1)
+  auto softmax = [&](int par, int h) __attribute__((always_inline)) {
+    const int j = NB == 2 ? h : 0, r0 = NB == 2 ? 0 : 8 * h, r1 = NB == 2 ? 16 : 8 * h + 8;
+#pragma unroll
+    for (int r = r0; r < r1; ++r) s[par][j][r] = fast_exp2(s[par][j][r]) * dp[par][j][r];
+    if (NB == 2 || h == 1) ds[par][j] = XOp<T>(s[par][j]);
+  };
+
+  {  // stage NST-1 stands in for tile -1
+    uint4* z = reinterpret_cast<uint4*>(smem + (NST - 1) * STAGE_BYTES);
+    for (int i = tid; i < STAGE_BYTES / 16; i += 64 * NW) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  if (VD_SP_PRIO && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  vm_drain();
+  issue(0);
+  issue(1);
+  readG(NST - 1, 0);
+  auto step = [&](int t, auto sg_c) __attribute__((always_inline)) {
+    constexpr int SG = decltype(sg_c)::value, SP = (SG + NST - 1) % NST;
+    vm_wait_barrier<PER_TILE>();  // tile t landed; tile t-2 no longer read
+    issue(t + 2);
+    VD_SP_FENCE();
+    readS(SG, 0);                 // R:S(b0)
+    VD_SP_FENCE();
+    mmaG(0);                      // M:G(b0-2) + the first half of V(b0-1)
+    softmax(1, 0);
+    sp_interleave<NMG, VD_SP_NV>();
+    VD_SP_FENCE();
+    readG(SP, 32);                // R:G(b0-1)
+    VD_SP_FENCE();
+    mmaS(0);                      // M:S(b0) + the second half of V(b0-1)
+    softmax(1, 1);
+    sp_interleave<NMS, VD_SP_NV>();
+    VD_SP_FENCE();
+    readS(SG, 32);                // R:S(b1)
+    VD_SP_FENCE();
+    mmaG(1);                      // M:G(b0-1) + V(b0), first half
+    softmax(0, 0);
+    sp_interleave<NMG, VD_SP_NV>();
+    VD_SP_FENCE();
+    readG(SG, 0);                 // R:G(b0)
+    VD_SP_FENCE();
+    mmaS(1);                      // M:S(b1) + V(b0), second half
+    softmax(0, 1);
+    sp_interleave<NMS, VD_SP_NV>();
+    VD_SP_FENCE();
+  };
+  const int nt = (ntiles + NST - 1) / NST * NST;  // zero K / V tiles past the end add nothing
+  for (int t = 0; t < nt; t += NST) {
+    step(t, std::integral_constant<int, 0>{});
+    step(t + 1, std::integral_constant<int, 1>{});
+    step(t + 2, std::integral_constant<int, 2>{});
+    step(t + 3, std::integral_constant<int, 3>{});
+  }
+  softmax(1, 0);  // V(2nt-1), then G(2nt-2) (fragments already read), G(2nt-1)
+  softmax(1, 1);
+  mmaG(0);
+  readG((nt - 1) & (NST - 1), 32);
+  mmaG(1);
+  vm_drain();
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    f32x16 out[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) out[i] = acc[i][j];
+    store_transposed<T, D / 32>(dq + base, ts, q0 + 32 * j + (lane & 31), n, 0, out, scale, lane);
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 int check_attn(const vd_attn_desc* d) {
   VD_REQUIRE(d, "null descriptor");
@@ -2020,8 +2438,10 @@ int check_attn(const vd_attn_desc* d) {
 //   kRole: head_dim-256 dK/dV with role-split wave pairs (attn_bwd_dkdv_role_kernel)
 //   kP4N2: the pipelined backward kernels with 4 waves x 2 blocks (one wave per SIMD,
 //          each LDS fragment feeds two MFMAs; bf16, D = 64; fwd keeps its default)
+//   kSP: the fragment-pipelined backward kernels (attn_bwd_dq_sp_kernel /
+//          attn_bwd_dkdv_sp_kernel; bf16, D = 64, >= 16 key tiles; fwd keeps its default)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
-               kPair = 8, kP4N2 = 9, kRole = 10, kCfgLast = kRole };
+               kPair = 8, kP4N2 = 9, kRole = 10, kSP = 11, kCfgLast = kSP };
 
 int cfg_from_env() {
   const char* e = getenv("VDIFF_ATTN_CFG");
@@ -2037,6 +2457,7 @@ int cfg_from_env() {
   if (!strcmp(e, "pair")) return (int)kPair;
   if (!strcmp(e, "p4n2")) return (int)kP4N2;
   if (!strcmp(e, "role")) return (int)kRole;
+  if (!strcmp(e, "sp")) return (int)kSP;
   return -1;
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
@@ -2055,6 +2476,7 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
+      !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
@@ -2276,6 +2698,51 @@ int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
   return vd::check_launch("attn_bwd_dq");
 }
 
+// fragment-pipelined backward (kSP): NW waves x NB x 32 rows per workgroup
+#ifndef VD_SP_NW
+#define VD_SP_NW 8
+#endif
+#ifndef VD_SP_NB
+#define VD_SP_NB 1
+#endif
+template <int D, int NW = VD_SP_NW, int NB = VD_SP_NB>
+int dq_sp_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                 const void* dout, const float* nlse2, const float* ndelta, void* dq,
+                 hipStream_t st) {
+  const size_t lds = tile_pipe_lds<D, false>();
+  auto kern = attn_bwd_dq_sp_kernel<D, NW, NB>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW * NB), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                               (const bf16_t*)dout, nlse2, ndelta, (bf16_t*)dq, d->seq_len,
+                               SeqAddr{d->batch_stride, d->group_stride, d->groups},
+                               d->token_stride,
+                               SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
+                               d->o_token_stride, d->scale);
+  return vd::check_launch("attn_bwd_dq");
+}
+template <int D, int NW = VD_SP_NW, int NB = VD_SP_NB>
+int dkdv_sp_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                   const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
+                   hipStream_t st) {
+  const size_t lds = tile_pipe_lds<D, true>();
+  auto kern = attn_bwd_dkdv_sp_kernel<D, NW, NB>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW * NB), (unsigned)d->nseq);
+  kern<<<grid, 64 * NW, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                               (const bf16_t*)dout, nlse2, ndelta, (bf16_t*)dk, (bf16_t*)dv,
+                               d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
+                               d->token_stride,
+                               SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
+                               d->o_token_stride, d->scale);
+  return vd::check_launch("attn_bwd_dkdv");
+}
+// the fragment-pipelined kernels round the tile count up to the ring's 4 stages: shorter
+// sequences keep the 8-wave pipelines
+inline bool sp_ok(const vd_attn_desc* d) { return d->seq_len >= 16 * kTile; }
+
 template <typename T, int D>
 int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
                 const void* v, const void* o, const void* dout, const float* lse, void* dq,
@@ -2297,7 +2764,9 @@ int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, con
     if constexpr (D == 64 || D == 128)
       if (c == kW8) return dq_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
-      if (c == kP8) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+      if (c == kSP && sp_ok(d)) return dq_sp_launch<D>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D == 64)
+      if (c == kP8 || c == kSP) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kP4N2) return dq_pipe_launch<T, D, 4, 2>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D <= 128)
@@ -2422,7 +2891,11 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
     if constexpr (D == 64 || D == 128)
       if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
-      if (c == kP8) return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+      if (c == kSP && sp_ok(d))
+        return dkdv_sp_launch<D>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 64)
+      if (c == kP8 || c == kSP)
+        return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kP4N2)
         return dkdv_pipe_launch<T, D, 4, 2>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);

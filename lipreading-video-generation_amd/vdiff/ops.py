@@ -859,12 +859,13 @@ def cross_attention(q, kv, heads=1, frames=1, per_frame=True):
 
 
 ATTN_CONFIGS = {"auto": -1, "base": 0, "nb2": 1, "w8": 2, "p8": 3, "p4": 4, "d8": 5, "d8n": 6, "d4": 7,
-                "pair": 8, "p4n2": 9, "role": 10}
+                "pair": 8, "p4n2": 9, "role": 10, "sp": 11}
 
 
 class attention_config:
     """Context manager selecting the bf16 attention kernel shape (vd_attention_set_config):
-    "auto" (per-kernel default), "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair".  Results agree across
+    "auto" (per-kernel default), "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair",
+    "p4n2", "role", "sp".  Results agree across
     shapes up to fp32 summation order; used by tests and A/B benchmarks."""
 
     def __init__(self, name: str):

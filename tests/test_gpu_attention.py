@@ -65,7 +65,8 @@ def test_scores_with_large_logits():
     assert rel_l2(out, ref) < 2e-5
 
 
-CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair", "p4n2", "role"]
+CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair", "p4n2", "role",
+           "sp"]
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
@@ -127,7 +128,7 @@ def test_bf16_lagged_max_rescale_default_shapes(C):
 
 def test_config_hook_rejects_unknown():
     from vdiff import _lib, ops
-    assert _lib.lib().vd_attention_set_config(11) == -2
+    assert _lib.lib().vd_attention_set_config(12) == -2
     with pytest.raises(ValueError):
         ops.attention_config("fast")
 
