@@ -1561,13 +1561,23 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
 #ifndef VD_DEFER_MSUM
 #define VD_DEFER_MSUM 0
 #endif
+// VD_DEFER_B2 (A/B, D = 64 with 8 waves): an 8-stage ring with one barrier per TWO tiles
+// (prefetch distance 4, two tiles issued per barrier), so the SIMD partners re-align at
+// half as many barriers.
+#ifndef VD_DEFER_B2
+#define VD_DEFER_B2 0
+#endif
+template <int D, int NW> constexpr bool defer_b2() { return VD_DEFER_B2 && D == 64 && NW == 8; }
+template <int D, int NW> constexpr int defer_nst() { return defer_b2<D, NW>() ? 8 : 4; }
+
 template <typename T, int D, int NW, bool STAGGER>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   static_assert(kDMA<T> && (D == 64 || D == 128), "deferred-check forward: bf16, D = 64 / 128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TE = kTile * D, NST = 4, PD = 2;
+  constexpr bool B2 = defer_b2<D, NW>();
+  constexpr int TE = kTile * D, NST = defer_nst<D, NW>(), PD = B2 ? 4 : 2;
   constexpr int STAGE_BYTES = pipe_stage_bytes<D, false, kTile>();
   constexpr int PER_TILE = 2 * dma_ipw<D, NW, kTile>();
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
@@ -1732,8 +1742,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     constexpr int SG = decltype(sg_c)::value;
     const char* cur = SG >= 0 ? smem + SG * STAGE_BYTES : nullptr;
     const char* prv = SG >= 0 ? smem + ((SG + NST - 1) % NST) * STAGE_BYTES : nullptr;
-    vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
-    issue(t + PD);
+    if constexpr (B2) {  // even tiles: t, t+1 landed; t-4, t-3 no longer read
+      if (SG >= 0 ? (SG & 1) == 0 : (t & 1) == 0) {
+        vm_wait_barrier<2 * PER_TILE>();
+        issue(t + PD);
+        issue(t + PD + 1);
+      }
+    } else {
+      vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
+      issue(t + PD);
+    }
     const int b0 = 2 * t;
     if constexpr (LATE) V(sb, pb, psb, b0 - 1, std::false_type{});
     check(t - 1);
@@ -1794,6 +1812,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
       tile(t + 1, late_c, std::false_type{}, std::integral_constant<int, 1>{});
       tile(t + 2, late_c, std::false_type{}, std::integral_constant<int, 2>{});
       tile(t + 3, late_c, std::false_type{}, std::integral_constant<int, 3>{});
+      if constexpr (NST == 8) {
+        tile(t + 4, late_c, std::false_type{}, std::integral_constant<int, 4>{});
+        tile(t + 5, late_c, std::false_type{}, std::integral_constant<int, 5>{});
+        tile(t + 6, late_c, std::false_type{}, std::integral_constant<int, 6>{});
+        tile(t + 7, late_c, std::false_type{}, std::integral_constant<int, 7>{});
+      }
     }
 #endif
     for (; t < ntiles - 1; ++t) tile(t, late_c, std::false_type{}, Dyn{});
@@ -2614,7 +2638,7 @@ int fwd_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const v
 template <typename T, int D, int NW, bool STAGGER>
 int fwd_defer_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
                      float* lse, hipStream_t st) {
-  const size_t lds = tile_pipe_lds<D, false>();
+  const size_t lds = (size_t)defer_nst<D, NW>() * pipe_stage_bytes<D, false, kTile>();
   auto kern = attn_fwd_defer_kernel<T, D, NW, STAGGER>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
