@@ -1,0 +1,18 @@
+#!/bin/bash
+# End-of-session measurement set (GPU box): the full GPU test suite, the default bench.py
+# line, then rocprofv3 --kernel-trace --stats of the very same bench.py invocation.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/pytest_gpu_final.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_final.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu_final.log
+timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 900 python -u bench.py > gpurun_out/r02b_bench.json 2> gpurun_out/r02b_bench.err || { tail -20 gpurun_out/r02b_bench.err; exit 1; }
+tail -c 400 gpurun_out/r02b_bench.json
+rm -rf /tmp/prof_r02b
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/prof_r02b -o run -- \
+  python -u bench.py > gpurun_out/r02b_bench_profiled.json 2> gpurun_out/r02b_bench_profiled.err || { tail -20 gpurun_out/r02b_bench_profiled.err; exit 1; }
+db=$(find /tmp/prof_r02b -name '*.db' | head -n 1)
+python tools/prof_summary.py "$db" > gpurun_out/r02b_kernel_stats.md
+head -12 gpurun_out/r02b_kernel_stats.md
