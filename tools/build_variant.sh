@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../lipreading-video-generation_amd/csrc"
 make -s -j8 >/dev/null
 NAME=$1; shift
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function \
-  -munsafe-fp-atomics -I../../include -mllvm -amdgpu-mfma-vgpr-form=1 $@ -c attention.hip \
+  -munsafe-fp-atomics -I../../include -mllvm -amdgpu-mfma-vgpr-form=1 -fno-slp-vectorize $@ -c attention.hip \
   -o build/attention_$NAME.o
 OBJS=$(ls build/*.o | grep -v -e "attention" -e "/conv_")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../vdiff/libvdiff_$NAME.so $OBJS build/attention_$NAME.o
