@@ -1561,6 +1561,9 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
 #ifndef VD_DEFER_MSUM
 #define VD_DEFER_MSUM 0
 #endif
+#ifndef VD_DEFER_TREE
+#define VD_DEFER_TREE 1
+#endif
 // VD_DEFER_B2 (A/B, D = 64 with 8 waves): an 8-stage ring with one barrier per TWO tiles
 // (prefetch distance 4, two tiles issued per barrier), so the SIMD partners re-align at
 // half as many barriers.
@@ -1661,12 +1664,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
 #else
   auto V = [&](f32x16& s, XOp<T>& p, float& ps, int bi, auto mk) __attribute__((always_inline)) {
     if constexpr (decltype(mk)::value) mask(s, bi);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = fast_exp2(s[r]);
+#if VD_DEFER_TREE
+    // pairwise: a 4-deep dependency chain instead of 16 (A/B build flag)
+    float t8[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) t8[r] = s[2 * r] + s[2 * r + 1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t8[r] = t8[2 * r] + t8[2 * r + 1];
+    ps = (t8[0] + t8[1]) + (t8[2] + t8[3]);
+#else
     ps = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[r] = fast_exp2(s[r]);
-      ps += s[r];
-    }
+    for (int r = 0; r < 16; ++r) ps += s[r];
+#endif
     p = XOp<T>(s);
   };
 #endif
