@@ -17,13 +17,17 @@ windows of 4000 samples) per GPU, resident in HBM before timing.  A step = q_sam
 Secondary: DDIM steps/sec = one 50-step-DDIM denoising step (UNet forward at
 B=1 + DDIM update) on the same model, audio encoded once per clip.
 
-roofline: the flash-attention kernel with the largest share of the timed train
-step, timed per launch with HIP events on its launch stream; FLOP per launch is
-the algorithmic count (vdiff.flops.attention_kernel_flops); peak = 2.5 PF/s bf16
-dense (MI355X_MICROARCH.md).  traffic: HBM bytes per launch from the committed
+roofline: the flash-attention UNIT with the largest share of the timed train step
+(the forward launch, or the dQ + dK/dV launch pair of the backward), timed per launch
+with HIP events on its launch stream; FLOP per unit is the algorithmic count of SURVEY
+8(d) (vdiff.flops.attention_unit_flops: forward 4 N^2 D, backward 8 N^2 D, no credit
+for recompute; executed_frac counts the products the kernels run); peak = 2.5 PF/s
+bf16 dense (MI355X_MICROARCH.md).  traffic: HBM bytes per unit from the committed
 rocprofv3 PMC summary (profiles/pmc_traffic.json) if present, else null.
 cpu_baseline: the oracle (fp32 torch-CPU restatement of the reference) train step
-on a bounded sample, scaled by algorithmic FLOP to the workload (see "sample").
+timed on the host cores as BASELINE.md section 3 plans -- the config-2 model in
+spatial_temporal mode on a bounded 2-frame clip, and config 1 (tiny UNet3D, joint);
+no FLOP extrapolation (see "sample").
 """
 from __future__ import annotations
 
