@@ -1571,6 +1571,20 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
 #define VD_DEFER_B2 0
 #endif
 template <int D, int NW> constexpr bool defer_b2() { return VD_DEFER_B2 && D == 64 && NW == 8; }
+// VD_DEFER_IGLP (A/B): the softmax of block 2t (V(sa)) spread over the MFMAs of S(2t+1) and
+// G(2t-1) -- NV VALU per MFMA (sched_group_barrier), the region fenced by sched_barriers --
+// instead of the compiler's clusters of 6-7 v_exp between two MFMAs.
+#ifndef VD_DEFER_IGLP
+#define VD_DEFER_IGLP 0
+#endif
+template <int NM, int NV>
+__device__ __forceinline__ void defer_interleave() {
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+  }
+}
 template <int D, int NW> constexpr int defer_nst() { return defer_b2<D, NW>() ? 8 : 4; }
 
 template <typename T, int D, int NW, bool STAGGER>
@@ -1807,9 +1821,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
 #else
     S(sa, b0, cur);
     G(pa, b0 - 2, prv);
+    if constexpr (VD_DEFER_IGLP && D == 64 && !decltype(mk)::value) __builtin_amdgcn_sched_barrier(0);
     V(sa, pa, psa, b0, mk);
     S(sb, b0 + 1, cur);
     G(pb, b0 - 1, prv);
+    if constexpr (VD_DEFER_IGLP && D == 64 && !decltype(mk)::value) {
+      defer_interleave<2 * (D / 16), VD_DEFER_IGLP>();
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #endif
     if constexpr (!LATE) V(sb, pb, psb, b0 + 1, mk);
   };
