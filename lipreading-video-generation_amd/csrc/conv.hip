@@ -1251,6 +1251,258 @@ void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, c
                                     ca, (const bf16_t*)res);
 }
 
+// ----------------------------------------------------------------- 3x3x3 stride 1: halo tile
+// The gathered-tile kernel above DMAs every tap's A tile separately: for 64 output channels
+// that is 4 of the 5 LDS-DMA pieces a wave issues per 32 MFMAs (and ~60 cycles of issue each,
+// MI355X_MICROARCH.md), so the 64-channel convs are DMA-issue bound.  Here a workgroup owns an
+// output tile of 2 x 4 x 16 pixels (t, h, w) x 64 channels; per 64-channel step the input
+// halo of the tile (4 x 6 x 18 pixels, 54 KiB) lands in LDS once, and all 27 taps read their
+// A fragments from it at shifted pixel offsets (16 consecutive w per fragment row group: with
+// the chunk swizzle of ig_off the 16 lanes hit 16 distinct bank quads for any shift).  Only
+// each tap's 64 x 64 weight slice (8 KiB) streams, through a 3-stage ring.  Pieces per wave
+// per tap: 2 (weights) + 14 / 27 (halo).  Transposed (bwd-data, stride 1): the same halo with
+// the tap offsets mirrored (source pixel = out + 1 - tap).  Needs W % 16 == 0; partial t / h
+// tiles are masked (zero halo rows, skipped stores).
+constexpr int kHoT = 2, kHoH = 4, kHoW = 16;                    // output tile
+constexpr int kHaT = kHoT + 2, kHaH = kHoH + 2, kHaW = kHoW + 2;  // input halo
+constexpr int kHaP = kHaT * kHaH * kHaW;                         // 432 pixels = 54 pieces
+constexpr int kHaBytes = kHaP * 128;
+// weight ring stages (prefetch distance NSTB - 1); VDIFF_CONV_HALO_ST selects 3 (two
+// workgroups per CU: 80 KiB of LDS each) or 5 / 7 (one workgroup per CU)
+template <int NSTB>
+constexpr size_t halo_lds() { return kHaBytes + NSTB * 64 * 128 + 2048; }  // + a throw-away slot
+static_assert(kHaP % 8 == 0, "whole halo pieces");
+
+template <bool TR, int NSTB, int NW>
+__global__ __launch_bounds__(64 * NW, NSTB <= 3 ? 2 : 1) void halo_conv_kernel(
+    GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
+    bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
+    const bf16_t* __restrict__ residual) {
+  // NW waves: each owns NI = 8 / NW fragment rows (16 output pixels each) of the 128-pixel tile
+  constexpr int BN = 64, NI = 8 / NW, NJ = 4, IB = 8 / NW, TAPS = 27;
+  constexpr int HPW = (kHaP / 8 + NW - 1) / NW;  // halo pieces per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bf16_t* halo = reinterpret_cast<const bf16_t*>(smem);
+  char* ring = smem + kHaBytes;
+  constexpr int PD = NSTB - 1;
+  char* junk = ring + NSTB * BN * 128;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesW = g.dW / kHoW, tilesH = (g.dH + kHoH - 1) / kHoH;
+  const int tilesT = (g.dT + kHoT - 1) / kHoT;
+  int mt = blockIdx.x;
+  const int w0 = (mt % tilesW) * kHoW;
+  mt /= tilesW;
+  const int h0 = (mt % tilesH) * kHoH;
+  mt /= tilesH;
+  const int t0 = (mt % tilesT) * kHoT;
+  const int b = mt / tilesT;
+  const int n0 = blockIdx.y * BN;
+  const int C = g.sC, csteps = (C + kIgBK - 1) / kIgBK;
+  const int lr = lane >> 3, pc = lane & 7;
+  const rsrc_t rs_a = make_rsrc(src, (uint32_t)((int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2));
+  const rsrc_t rs_b = make_rsrc(wt, (uint32_t)((int64_t)g.N * g.K * 2));
+
+  // this wave's halo pieces q = wave + 4 i: pixel p = 8 q + lane / 8, physical chunk lane % 8
+  int h_off[HPW], h_c[HPW];
+#pragma unroll
+  for (int i = 0; i < HPW; ++i) {
+    const int q = wave + NW * i, p = 8 * q + lr;
+    const int c = pc ^ ((p >> 1) & 7);
+    const int hw = p % kHaW, hh = (p / kHaW) % kHaH, ht = p / (kHaW * kHaH);
+    const int st = t0 - 1 + ht, sh = h0 - 1 + hh, sw = w0 - 1 + hw;
+    const bool in = q < kHaP / 8 && (unsigned)st < (unsigned)g.sT &&
+                    (unsigned)sh < (unsigned)g.sH && (unsigned)sw < (unsigned)g.sW;
+    h_off[i] = in ? (((b * g.sT + st) * g.sH + sh) * g.sW + sw) * g.sCs * 2 + c * 16 : -1;
+    h_c[i] = c * 8;
+  }
+  auto issue_halo = [&](int cs) {
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int q = wave + NW * i;
+      const bool ok = (h_off[i] >= 0) & (cs * kIgBK + h_c[i] < C);
+      dma_lds<16>(rs_a, lds_addr(q < kHaP / 8 ? smem + q * 1024 : junk),
+                  ok ? (uint32_t)(h_off[i] + cs * kIgBK * 2) : 0x80000000u);
+    }
+  };
+  int b_off[IB], b_c[IB];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int r = (wave * IB + i) * 8 + lr;
+    const int c = pc ^ ((r >> 1) & 7);
+    b_c[i] = c * 8;
+    const int n = n0 + r;
+    b_off[i] = n < g.N ? n * g.K * 2 + c * 16 : -1;
+  }
+  auto issue_b = [&](int cs, int tap) {  // tap >= 27: zero fill into the free stage
+    char* st = ring + (tap % NSTB) * (BN * 128);
+    const int c0 = cs * kIgBK;
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const bool ok = (tap < TAPS) & (b_off[i] >= 0) & (c0 + b_c[i] < C);
+      dma_lds<16>(rs_b, lds_addr(st + (wave * IB + i) * 1024),
+                  ok ? (uint32_t)(b_off[i] + (tap * C + c0) * 2) : 0x80000000u);
+    }
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  // the wave's two fragment rows: output rows (t_l, h_l) = blocks 2 wave, 2 wave + 1
+  int prow[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int rb = NI * wave + i, tl = rb / kHoH, hl = rb % kHoH;
+    prow[i] = (tl * kHaH + hl) * kHaW + fr;  // halo pixel of tap (0, 0, 0) (fwd orientation)
+  }
+
+  vm_drain();
+  for (int cs = 0; cs < csteps; ++cs) {
+    __syncthreads();  // every wave is done with the previous step's halo and ring
+    issue_halo(cs);
+#pragma unroll
+    for (int i = 0; i < PD; ++i) issue_b(cs, i);
+    for (int tap = 0; tap < TAPS; ++tap) {
+      // this tap's weights (and at tap 0 the halo) landed everywhere; stage tap-1 is free
+      vm_wait_barrier<(PD - 1) * IB>();
+      issue_b(cs, tap + PD);
+      const int a = tap / 9, bb = (tap / 3) % 3, cc = tap % 3;
+      const int dt = TR ? 2 - a : a, dh = TR ? 2 - bb : bb, dw = TR ? 2 - cc : cc;
+      const int shift = (dt * kHaH + dh) * kHaW + dw;
+      const bf16_t* Bs = reinterpret_cast<const bf16_t*>(ring + (tap % NSTB) * (BN * 128));
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[NI], bfr[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(halo + ig_off(prow[i] + shift, 4 * s + fq));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ig_off(16 * j + fr, 4 * s + fq));
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  vm_drain();  // the zero-fill pieces past the last tap land before the epilogue reuses LDS
+  __syncthreads();
+
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int LDC = BN + 4;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(16 * (NI * wave + i) + fq * 4 + r) * LDC + 16 * j + fr] = acc[i][j][r];
+  __syncthreads();
+  const bool vec = (g.N % 8 == 0) && (g.dNs % 8 == 0);
+  for (int v = tid; v < 128 * BN / 8; v += 64 * NW) {
+    const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+    const int t = t0 + r / (kHoH * kHoW), h = h0 + (r / kHoW) % kHoH, w = w0 + r % kHoW;
+    const int n = n0 + c;
+    if (t >= g.dT || h >= g.dH || n >= g.N) continue;
+    const int64_t m = (((int64_t)b * g.dT + t) * g.dH + h) * g.dW + w;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
+    const int lim = g.N - n < 8 ? g.N - n : 8;
+    if (bias)
+      for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
+    if (chan_add)
+      for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)b * g.N + n + e];
+    bf16_t* out = dst + m * g.dNs + n;
+    if (vec) {
+      if (residual) {
+        float rv[8];
+        load8(residual + m * g.dNs + n, rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rv[e];
+      }
+      store8(out, o);
+    } else {
+      for (int e = 0; e < lim; ++e) {
+        float val = o[e];
+        if (residual) val += bf2f(residual[m * g.dNs + n + e]);
+        out[e] = f2bf(val);
+      }
+    }
+  }
+}
+
+// halo-tile eligibility: 3x3x3, stride 1, pad 1, same-size in / out, W a multiple of 16
+bool halo_ok(const GemmGeom& g) {
+  return g.kt == 3 && g.kh == 3 && g.kw == 3 && g.st == 1 && g.sh == 1 && g.sw == 1 &&
+         g.pt == 1 && g.ph == 1 && g.pw == 1 && g.sT == g.dT && g.sH == g.dH && g.sW == g.dW &&
+         g.dW % kHoW == 0;
+}
+// VDIFF_CONV_HALO: 0 never, 1 every eligible conv, 2 (default) where it measured faster.
+// Same-box per-shape A/B over the config-2 train step (profiles/r02_ab_conv_halo.txt): the
+// halo tile wins for N <= 64 (fwd 200->64 / 192->64 0.66x, 64->64 0.87x, bwd-data 64->64
+// 0.84x) and at the 32x32 level up to N = 256 (0.68-0.83x); with N >= 128 at 64x64 and
+// 128x128 the gathered 128 x 128 tiles keep the edge (1.0-1.1x): the halo kernel's N tile is
+// 64, so every 64 output channels re-load the halo.  Deeper weight rings (one workgroup per
+// CU) and 8 waves per workgroup measured slower (VDIFF_CONV_HALO_ST / _NW).
+int conv_halo_mode() {
+  static const int v = [] {
+    const char* e = getenv("VDIFF_CONV_HALO");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+bool halo_use(const GemmGeom& g) {
+  const int m = conv_halo_mode();
+  if (m == 0 || !halo_ok(g)) return false;
+  return m == 1 || g.N <= 64 || (g.dW <= 32 && g.N <= 256);
+}
+template <bool TR, int NSTB, int NW>
+void launch_halo_st(const GemmGeom& g, const void* src, const void* wt, void* dst,
+                    const float* bias, const float* ca, const void* res, hipStream_t st) {
+  const size_t lds_c = (size_t)128 * (64 + 4) * 4;
+  const size_t lds = halo_lds<NSTB>() > lds_c ? halo_lds<NSTB>() : lds_c;
+  auto kern = halo_conv_kernel<TR, NSTB, NW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  const int64_t tiles = (int64_t)g.B * vd_cdiv(g.dT, kHoT) * vd_cdiv(g.dH, kHoH) * (g.dW / kHoW);
+  dim3 grid((unsigned)tiles, (unsigned)vd_cdiv(g.N, 64));
+  kern<<<grid, 64 * NW, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias,
+                                   ca, (const bf16_t*)res);
+}
+int conv_halo_waves() {
+  static const int v = [] {
+    const char* e = getenv("VDIFF_CONV_HALO_NW");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+int conv_halo_stages() {
+  static const int v = [] {
+    const char* e = getenv("VDIFF_CONV_HALO_ST");
+    return e ? atoi(e) : 3;
+  }();
+  return v;
+}
+template <bool TR>
+void launch_halo(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
+                 const float* ca, const void* res, hipStream_t st) {
+  const int ns = conv_halo_stages();
+  if (conv_halo_waves() == 8) {
+    if (ns == 5) launch_halo_st<TR, 5, 8>(g, src, wt, dst, bias, ca, res, st);
+    else launch_halo_st<TR, 3, 8>(g, src, wt, dst, bias, ca, res, st);
+  } else {
+    if (ns == 5) launch_halo_st<TR, 5, 4>(g, src, wt, dst, bias, ca, res, st);
+    else launch_halo_st<TR, 3, 4>(g, src, wt, dst, bias, ca, res, st);
+  }
+}
+
 // ----------------------------------------------------------------- 1x1 convs: streaming GEMM
 // A 1x1, stride-1, unpadded conv (qkv / proj_out / skip, fwd and bwd-data) is an HBM-bound
 // GEMM over pixels: Y[p][n] = sum_k X[p][k] W[n][k] with K = 32 KS <= 256 and a weight slice
@@ -1507,8 +1759,13 @@ int launch_gemm(const GemmGeom& g, const void* src, const void* wt, void* dst, c
     // when transposed
     if (!g_legacy_conv && g_conv_dma && g.kt * g.kh * g.kw <= 32 && (!TR || unit) &&
         (int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2 < ((int64_t)1 << 31) &&
-        (int64_t)g.N * g.K * 2 < ((int64_t)1 << 31))
+        (int64_t)g.N * g.K * 2 < ((int64_t)1 << 31)) {
+      if (halo_use(g)) {
+        launch_halo<TR>(g, src, wt, dst, bias, ca, res, st);
+        return VD_OK;
+      }
       return launch_igemm_dma<TR>(g, src, wt, dst, bias, ca, res, st);
+    }
     if (!g_legacy_conv) return launch_igemm<TR>(g, src, wt, dst, bias, ca, res, st);
   }
   const int64_t mt = vd_cdiv(g.M, 128);

@@ -29,6 +29,8 @@ CASES = [
     ((1, 96, 2, 5, 7), 48, 1, 1, 0),           # streaming 1x1: K = 96 (odd K step count)
     ((1, 256, 2, 6, 6), 768, 1, 1, 0),         # streaming 1x1: weight in 12 LDS slices
     ((1, 64, 1, 3, 7), 40, 1, 1, 0),           # 1x1 with N % 16 != 0: igemm fallback
+    ((2, 96, 3, 5, 32), 80, 3, 1, 1),          # halo tile: 2 channel steps, partial t / h, ragged N
+    ((1, 64, 2, 4, 16), 64, 3, 1, 1),          # halo tile: exact fit
 ]
 
 
@@ -71,13 +73,14 @@ def test_conv_fwd_bwd_vs_oracle(case, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_conv_fused_epilogue(dtype):
+@pytest.mark.parametrize("spatial", [(2, 7, 9), (3, 5, 16)])  # gathered tiles / halo tiles
+def test_conv_fused_epilogue(dtype, spatial):
     """y = conv(x) + bias + chan_add[b, co] + residual (the ResBlock emb-add and skip-add)."""
     from vdiff import ops
-    x = seeded((2, 64, 2, 7, 9), 1)
+    x = seeded((2, 64) + spatial, 1)
     w, b = _weights(64, 128, 3, 3, 2)
     ca = seeded((2, 128), 4)
-    res = seeded((2, 128, 2, 7, 9), 5)
+    res = seeded((2, 128) + spatial, 5)
     if dtype == torch.bfloat16:
         x, w, res = x.bfloat16().float(), w.bfloat16().float(), res.bfloat16().float()
     leaves = [t.clone().requires_grad_(True) for t in (x, w, b, ca, res)]
