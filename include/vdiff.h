@@ -192,6 +192,13 @@ int vd_conv3d_bwd_data(const vd_conv_desc* d, const void* dy,
 int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy,
                          float* dw, void* stream);
 
+/* Which 3x3x3 stride-1 bf16 convs (fwd / bwd-data) take the halo-tile kernel: 0 none, 1 every
+ * eligible shape (W % 16 == 0, pad 1), 2 (default) the shapes where it measured faster
+ * (N <= 64, or W <= 32 and N <= 256).  Results are identical up to fp32 summation order.
+ * Process-wide; returns the previous mode, or -2 for an invalid one.  Initial value from env
+ * VDIFF_CONV_HALO.  No reference counterpart: an A/B and test hook. */
+int vd_conv_set_halo(int mode);
+
 /* ---- Conv glue ---------------------------------------------------------
  * vd_channel_sums: out[b][c] = sum over the S pixels of x[b][s][c] (fp32; x channels-last
  * with pixel stride cstride, 0 = C; C % 8 == 0; deterministic two-stage reduction through

@@ -21,6 +21,8 @@
 #include "vd_common.h"
 #include <stdlib.h>
 
+#include <atomic>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -1451,13 +1453,11 @@ bool halo_ok(const GemmGeom& g) {
 // 128x128 the gathered 128 x 128 tiles keep the edge (1.0-1.1x): the halo kernel's N tile is
 // 64, so every 64 output channels re-load the halo.  Deeper weight rings (one workgroup per
 // CU) and 8 waves per workgroup measured slower (VDIFF_CONV_HALO_ST / _NW).
-int conv_halo_mode() {
-  static const int v = [] {
-    const char* e = getenv("VDIFF_CONV_HALO");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
+std::atomic<int> g_halo_mode{[] {
+  const char* e = getenv("VDIFF_CONV_HALO");
+  return e ? atoi(e) : 2;
+}()};
+int conv_halo_mode() { return g_halo_mode.load(std::memory_order_relaxed); }
 bool halo_use(const GemmGeom& g) {
   const int m = conv_halo_mode();
   if (m == 0 || !halo_ok(g)) return false;
@@ -1811,6 +1811,14 @@ int vd_conv3d_fwd(const vd_conv_desc* d, const void* x, const void* w_fwd, const
   return VD_DISPATCH_DTYPE(d->dtype, T, {
     launch_gemm<T, false>(g, x, w_fwd, y, bias, chan_add, residual, VD_STREAM(stream));
   });
+}
+
+int vd_conv_set_halo(int mode) {
+  if (mode < 0 || mode > 2) {
+    (void)vd::fail(VD_EINVAL, "conv halo mode %d (0, 1, 2)", mode);
+    return -2;
+  }
+  return g_halo_mode.exchange(mode);
 }
 
 int vd_conv3d_bwd_data(const vd_conv_desc* d, const void* dy, const void* w_bwd, void* dx,

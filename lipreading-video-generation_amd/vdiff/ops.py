@@ -885,6 +885,28 @@ class attention_config:
         return False
 
 
+class conv_halo:
+    """Context manager selecting which 3x3x3 stride-1 bf16 convs take the halo-tile kernel
+    (vd_conv_set_halo): 0 none, 1 every eligible shape, 2 (default) where it measured faster.
+    Results agree up to fp32 summation order; used by tests and A/B benchmarks."""
+
+    def __init__(self, mode: int):
+        if mode not in (0, 1, 2):
+            raise ValueError(f"conv halo mode {mode!r}: 0, 1 or 2")
+        self.mode = mode
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = _lib.lib().vd_conv_set_halo(self.mode)
+        if self.prev < 0:
+            raise RuntimeError(_lib.lib().vd_last_error().decode())
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().vd_conv_set_halo(self.prev)
+        return False
+
+
 def attention(qkv, heads=1, mode="joint", spatial=None, legacy=True):
     if mode != "joint" and spatial is None:
         raise ValueError("spatial/temporal attention needs the (T, H, W) shape")

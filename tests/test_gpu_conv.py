@@ -44,6 +44,31 @@ def _weights(Ci, Co, k, nd, seed):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_conv_fwd_bwd_vs_oracle(case, dtype):
+    _conv_vs_oracle(case, dtype)
+
+
+# every 3x3x3 stride-1 case that fits the halo tile (W % 16 == 0), on both kernels whatever
+# the default selection picks for it
+HALO_CASES = [i for i, c in enumerate(CASES)
+              if len(c[0]) == 5 and c[2] == 3 and c[3] == 1 and c[4] == 1 and c[0][-1] % 16 == 0]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_modes(case, mode):
+    from vdiff import ops
+    with ops.conv_halo(mode):
+        _conv_vs_oracle(case, torch.bfloat16)
+
+
+def test_conv_halo_hook_rejects_unknown():
+    from vdiff import _lib, ops
+    assert _lib.lib().vd_conv_set_halo(3) == -2
+    with pytest.raises(ValueError):
+        ops.conv_halo(5)
+
+
+def _conv_vs_oracle(case, dtype):
     from vdiff import ops
     shape, Co, k, stride, pad = CASES[case]
     nd = len(shape) - 2
