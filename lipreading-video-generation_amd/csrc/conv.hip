@@ -845,15 +845,19 @@ __device__ __forceinline__ int wg_off(int r, int c) {  // element offset of chan
   return r * 64 + ((((c >> 3) ^ wg_swz(r)) << 3) | (c & 7));
 }
 
-template <int RW, int COT, int NST, bool ONE>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
-__global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
+// PLANE (round 2): all nine (kh, kw) taps of one kt per workgroup -- the X strip holds the
+// three input rows above / at / below the step's 64-pixel output row (W % 64 == 0, so a step
+// is one row segment), and one dY tile feeds nine taps instead of three.
+template <int RW, int COT, int NST, bool ONE, bool PLANE = false>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
+__global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
     WgtGeom g, int wc, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
     float* __restrict__ dw) {
   constexpr int PY = COT / 32, PX = RW / 32;  // pieces per wave per step
   constexpr int PIECES = PY + PX;
   constexpr int Y_BYTES = COT * 128, STAGE = (COT + RW) * 128;
   constexpr int WTM = COT / 2, NI = WTM / 16;
-  constexpr int NT = ONE ? 1 : 3;  // taps per workgroup
+  constexpr int NT = ONE ? 1 : (PLANE ? 9 : 3);  // taps per workgroup
+  static_assert(!PLANE || RW >= 3 * 66, "plane: three strip rows of 66 pixels");
   static_assert(!ONE || RW == 64, "1x1: the X tile is the step's 64 pixels");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bf16_t* lds = reinterpret_cast<const bf16_t*>(smem);
@@ -862,8 +866,8 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
   int bid = blockIdx.x;
   const int cot = bid % co_tiles; bid /= co_tiles;
   const int cit = bid % ci_tiles; bid /= ci_tiles;
-  const int tab = bid;
-  const int ta = tab / g.kh, tb = tab % g.kh;
+  const int tab = bid;  // PLANE: kt index; otherwise (kt, kh) index
+  const int ta = PLANE ? tab : tab / g.kh, tb = PLANE ? 0 : tab % g.kh;
   const int co0 = cot * COT, ci0 = cit * 64;
   const int64_t mbeg = (int64_t)blockIdx.y * g.m_per_split;
   int64_t mend = mbeg + g.m_per_split;
@@ -897,7 +901,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
     }
     x_rr[i] = sr / SW;
     x_j[i] = sr - x_rr[i] * SW;
-    if (x_rr[i] >= R) x_rr[i] = -1;
+    if (x_rr[i] >= (PLANE ? 3 : R)) x_rr[i] = -1;
     x_col[i] = ci0 + (pc ^ wg_swz(sr)) * 8;
   }
   const rsrc_t rs_y = make_rsrc(dy, (uint32_t)(g.M * g.yCs * 2));
@@ -930,6 +934,13 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
       if (ONE) {
         if (live & (ms + x_j[i] < me) & (x_col[i] < g.Ci))
           off = (uint32_t)(((ms + x_j[i]) * g.xCs + x_col[i]) * 2);
+      } else if (PLANE) {  // strip row r: input row chh - 1 + r of the step's own frame
+        const int ti = ct - g.pt + ta, hi = chh - 1 + x_rr[i], wi = cw + x_j[i] - g.pw;
+        if (live & (x_rr[i] >= 0) & (x_col[i] < g.Ci) & ((unsigned)ti < (unsigned)g.Ti) &
+            ((unsigned)hi < (unsigned)g.Hi) & ((unsigned)wi < (unsigned)g.Wi)) {
+          const int pix = ((cb * g.Ti + ti) * g.Hi + hi) * g.Wi + wi;
+          off = (uint32_t)((pix * g.xCs + x_col[i]) * 2);
+        }
       } else if (live & (x_rr[i] >= 0) & (x_col[i] < g.Ci)) {
         int b = cb, t = ct, h = chh + x_rr[i];
         while (h >= g.Ho) {
@@ -1001,13 +1012,14 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
 #pragma unroll
       for (int tc = 0; tc < NT; ++tc) {
         bf16x8 bfr[2];
+        const int sh_t = PLANE ? (tc / 3) * SW + tc % 3 : tc;  // strip shift of the tap
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int c = wn * 32 + 16 * j + 4 * p4;
           const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(Xs + wg_off(s_lo + tc, c)));
+              (lds_bf16x4*)(Xs + wg_off(s_lo + sh_t, c)));
           const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(Xs + wg_off(s_hi + tc, c)));
+              (lds_bf16x4*)(Xs + wg_off(s_hi + sh_t, c)));
           bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
 #pragma unroll
@@ -1024,7 +1036,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_dma_kernel(
   const int64_t krow = (int64_t)taps * g.Ci;
 #pragma unroll
   for (int tc = 0; tc < NT; ++tc) {
-    const int tap = ONE ? 0 : tab * g.kw + tc;
+    const int tap = ONE ? 0 : (PLANE ? ta * 9 + tc : tab * g.kw + tc);
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -1878,21 +1890,28 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     const int wc = one ? 64 : (d->Wo < 64 ? d->Wo : 64);
     const int rows = one ? 64 : (64 / wc) * (wc + 2);
     const int cot = 64;
-    const int64_t tiles =
-        (int64_t)vd_cdiv(d->Co, cot) * vd_cdiv(d->Ci, 64) * (one ? 1 : d->kt * d->kh);
+    // nine-tap planes (VDIFF_CONV_WPLANE=1, A/B): image rows of whole 64-pixel steps
+    static const int wplane = [] {
+      const char* e = getenv("VDIFF_CONV_WPLANE");
+      return e ? atoi(e) : 0;
+    }();
+    const bool plane = !one && wplane && d->Wo % 64 == 0;
+    const int64_t tiles = (int64_t)vd_cdiv(d->Co, cot) * vd_cdiv(d->Ci, 64) *
+                          (one ? 1 : (plane ? d->kt : d->kt * d->kh));
     // ~2048 workgroups, but at least 32 K steps each for the strip kernel (shorter pixel
     // ranges lose more to the ring's fill and the atomic epilogue than they gain in
-    // occupancy: 64->64 at 128x128 0.13 -> 0.116 ms, tools/conv_ab.sh)
+    // occupancy: 64->64 at 128x128 0.13 -> 0.116 ms, tools/conv_ab.sh); planes do three
+    // times the MFMA work per step: at least 16 steps
     int64_t splits = vd_cdiv(2048, tiles);
-    int64_t maxs = vd_cdiv(g.M, one ? 1024 : 2048);
+    int64_t maxs = vd_cdiv(g.M, (one || plane) ? 1024 : 2048);
     if (splits > maxs) splits = maxs;
     if (splits < 1) splits = 1;
     g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
     splits = vd_cdiv(g.M, g.m_per_split);
     dim3 grid((unsigned)tiles, (unsigned)splits);
-#define VD_WGD(RW, COT, NST, ONE)                                                          \
+#define VD_WGD(RW, COT, NST, ONE, ...)                                                     \
   do {                                                                                     \
-    auto kern = wgrad_dma_kernel<RW, COT, NST, ONE>;                                       \
+    auto kern = wgrad_dma_kernel<RW, COT, NST, ONE, ##__VA_ARGS__>;                        \
     const int lds = NST * (COT + RW) * 128;                                                \
     (void)hipFuncSetAttribute((const void*)kern,                                           \
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
@@ -1901,6 +1920,7 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     // 64 x 64 tiles, double-buffered (40 KiB at RW = 96: three workgroups per CU).
     // Measured against COT = 128 and a three-stage ring: both slower (tools/conv_ab.sh).
     if (one) VD_WGD(64, 64, 2, true);
+    else if (plane) VD_WGD(224, 64, 2, false, true);
     else if (rows <= 96) VD_WGD(96, 64, 2, false);
     else if (rows <= 128) VD_WGD(128, 64, 2, false);
     else VD_WGD(192, 64, 2, false);

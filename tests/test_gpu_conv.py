@@ -31,6 +31,8 @@ CASES = [
     ((1, 64, 1, 3, 7), 40, 1, 1, 0),           # 1x1 with N % 16 != 0: igemm fallback
     ((2, 96, 3, 5, 32), 80, 3, 1, 1),          # halo tile: 2 channel steps, partial t / h, ragged N
     ((1, 64, 2, 4, 16), 64, 3, 1, 1),          # halo tile: exact fit
+    ((2, 96, 3, 5, 64), 80, 3, 1, 1),          # 64-pixel rows: wgrad planes, 2 ci tiles, ragged Co
+    ((1, 64, 2, 2, 128), 64, 3, 1, 1),         # two 64-pixel steps per row
 ]
 
 
