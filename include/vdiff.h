@@ -194,7 +194,8 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy,
 
 /* Which 3x3x3 stride-1 bf16 convs (fwd / bwd-data) take the halo-tile kernel: 0 none, 1 every
  * eligible shape (W % 16 == 0, pad 1), 2 (default) the shapes where it measured faster
- * (N <= 64, or W <= 32 and N <= 256).  Results are identical up to fp32 summation order.
+ * (32x32 level: N <= 256; larger levels: fwd N <= 128, bwd-data with <= 64 reduction
+ * channels or N <= 64).  Results are identical up to fp32 summation order.
  * Process-wide; returns the previous mode, or -2 for an invalid one.  Initial value from env
  * VDIFF_CONV_HALO.  No reference counterpart: an A/B and test hook. */
 int vd_conv_set_halo(int mode);

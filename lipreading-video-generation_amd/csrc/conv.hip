@@ -1280,26 +1280,41 @@ void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, c
 constexpr int kHoT = 2, kHoH = 4, kHoW = 16;                    // output tile
 constexpr int kHaT = kHoT + 2, kHaH = kHoH + 2, kHaW = kHoW + 2;  // input halo
 constexpr int kHaP = kHaT * kHaH * kHaW;                         // 432 pixels = 54 pieces
-constexpr int kHaBytes = kHaP * 128;
-// weight ring stages (prefetch distance NSTB - 1); VDIFF_CONV_HALO_ST selects 3 (two
-// workgroups per CU: 80 KiB of LDS each) or 5 / 7 (one workgroup per CU)
-template <int NSTB>
-constexpr size_t halo_lds() { return kHaBytes + NSTB * 64 * 128 + 2048; }  // + a throw-away slot
-static_assert(kHaP % 8 == 0, "whole halo pieces");
+// KS channels per step: 64 (128-B LDS rows, 80 KiB per workgroup, two per CU) or 32 (64-B
+// rows, 40 KiB, four per CU); weight ring stages NSTB (prefetch distance NSTB - 1):
+// VDIFF_CONV_HALO_KS / VDIFF_CONV_HALO_ST select them (A/B).
+template <int NSTB, int KS>
+constexpr size_t halo_lds() { return (size_t)(kHaP + NSTB * 64) * 2 * KS + 1024; }  // + junk
+static_assert(kHaP % 16 == 0, "whole halo pieces");
+// element offset of 16-B chunk c of row r: 128-B rows as ig_off, 64-B rows with the chunk
+// XOR (r >> 2) & 3 -- 16 consecutive rows at one chunk then cover all 16 bank quads
+template <int KS>
+__device__ __forceinline__ int ha_off(int r, int c) {
+  if constexpr (KS == 64) return ig_off(r, c);
+  else return r * 32 + ((c ^ ((r >> 2) & 3)) << 3);
+}
+template <int KS>
+__device__ __forceinline__ int ha_swz(int r) {
+  if constexpr (KS == 64) return (r >> 1) & 7;
+  else return (r >> 2) & 3;
+}
 
-template <bool TR, int NSTB, int NW>
-__global__ __launch_bounds__(64 * NW, NSTB <= 3 ? 2 : 1) void halo_conv_kernel(
+template <bool TR, int NSTB, int NW, int KS>
+__global__ __launch_bounds__(64 * NW, NSTB <= 3 ? (KS == 32 ? 4 : 2) : 1) void halo_conv_kernel(
     GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
     bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
     const bf16_t* __restrict__ residual) {
   // NW waves: each owns NI = 8 / NW fragment rows (16 output pixels each) of the 128-pixel tile
-  constexpr int BN = 64, NI = 8 / NW, NJ = 4, IB = 8 / NW, TAPS = 27;
-  constexpr int HPW = (kHaP / 8 + NW - 1) / NW;  // halo pieces per wave
+  constexpr int RB = 2 * KS, PPP = 1024 / RB, CPR = KS / 8;  // row bytes, rows per piece, chunks
+  constexpr int HP = kHaP / PPP;                                // halo pieces
+  constexpr int BN = 64, NI = 8 / NW, NJ = 4, IB = BN / PPP / NW, TAPS = 27;
+  constexpr int HPW = (HP + NW - 1) / NW;                       // halo pieces per wave
+  static_assert(IB >= 1, "one weight piece per wave at least");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bf16_t* halo = reinterpret_cast<const bf16_t*>(smem);
-  char* ring = smem + kHaBytes;
+  char* ring = smem + kHaP * RB;
   constexpr int PD = NSTB - 1;
-  char* junk = ring + NSTB * BN * 128;
+  char* junk = ring + NSTB * BN * RB;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1313,20 +1328,21 @@ __global__ __launch_bounds__(64 * NW, NSTB <= 3 ? 2 : 1) void halo_conv_kernel(
   const int t0 = (mt % tilesT) * kHoT;
   const int b = mt / tilesT;
   const int n0 = blockIdx.y * BN;
-  const int C = g.sC, csteps = (C + kIgBK - 1) / kIgBK;
-  const int lr = lane >> 3, pc = lane & 7;
+  const int C = g.sC, csteps = (C + KS - 1) / KS;
+  const int lr = lane / CPR, pc = lane % CPR;
   const rsrc_t rs_a = make_rsrc(src, (uint32_t)((int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2));
   const rsrc_t rs_b = make_rsrc(wt, (uint32_t)((int64_t)g.N * g.K * 2));
 
-  // this wave's halo pieces q = wave + 4 i: pixel p = 8 q + lane / 8, physical chunk lane % 8
+  // this wave's halo pieces q = wave + NW i: pixel p = PPP q + lane / CPR, physical chunk
+  // lane % CPR (it fetches the logical chunk that swizzles there)
   int h_off[HPW], h_c[HPW];
 #pragma unroll
   for (int i = 0; i < HPW; ++i) {
-    const int q = wave + NW * i, p = 8 * q + lr;
-    const int c = pc ^ ((p >> 1) & 7);
+    const int q = wave + NW * i, p = PPP * q + lr;
+    const int c = pc ^ ha_swz<KS>(p);
     const int hw = p % kHaW, hh = (p / kHaW) % kHaH, ht = p / (kHaW * kHaH);
     const int st = t0 - 1 + ht, sh = h0 - 1 + hh, sw = w0 - 1 + hw;
-    const bool in = q < kHaP / 8 && (unsigned)st < (unsigned)g.sT &&
+    const bool in = q < HP && (unsigned)st < (unsigned)g.sT &&
                     (unsigned)sh < (unsigned)g.sH && (unsigned)sw < (unsigned)g.sW;
     h_off[i] = in ? (((b * g.sT + st) * g.sH + sh) * g.sW + sw) * g.sCs * 2 + c * 16 : -1;
     h_c[i] = c * 8;
@@ -1335,23 +1351,23 @@ __global__ __launch_bounds__(64 * NW, NSTB <= 3 ? 2 : 1) void halo_conv_kernel(
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
       const int q = wave + NW * i;
-      const bool ok = (h_off[i] >= 0) & (cs * kIgBK + h_c[i] < C);
-      dma_lds<16>(rs_a, lds_addr(q < kHaP / 8 ? smem + q * 1024 : junk),
-                  ok ? (uint32_t)(h_off[i] + cs * kIgBK * 2) : 0x80000000u);
+      const bool ok = (h_off[i] >= 0) & (cs * KS + h_c[i] < C);
+      dma_lds<16>(rs_a, lds_addr(q < HP ? smem + q * 1024 : junk),
+                  ok ? (uint32_t)(h_off[i] + cs * KS * 2) : 0x80000000u);
     }
   };
   int b_off[IB], b_c[IB];
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
-    const int r = (wave * IB + i) * 8 + lr;
-    const int c = pc ^ ((r >> 1) & 7);
+    const int r = (wave * IB + i) * PPP + lr;
+    const int c = pc ^ ha_swz<KS>(r);
     b_c[i] = c * 8;
     const int n = n0 + r;
     b_off[i] = n < g.N ? n * g.K * 2 + c * 16 : -1;
   }
   auto issue_b = [&](int cs, int tap) {  // tap >= 27: zero fill into the free stage
-    char* st = ring + (tap % NSTB) * (BN * 128);
-    const int c0 = cs * kIgBK;
+    char* st = ring + (tap % NSTB) * (BN * RB);
+    const int c0 = cs * KS;
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const bool ok = (tap < TAPS) & (b_off[i] >= 0) & (c0 + b_c[i] < C);
@@ -1387,16 +1403,16 @@ __global__ __launch_bounds__(64 * NW, NSTB <= 3 ? 2 : 1) void halo_conv_kernel(
       const int a = tap / 9, bb = (tap / 3) % 3, cc = tap % 3;
       const int dt = TR ? 2 - a : a, dh = TR ? 2 - bb : bb, dw = TR ? 2 - cc : cc;
       const int shift = (dt * kHaH + dh) * kHaW + dw;
-      const bf16_t* Bs = reinterpret_cast<const bf16_t*>(ring + (tap % NSTB) * (BN * 128));
+      const bf16_t* Bs = reinterpret_cast<const bf16_t*>(ring + (tap % NSTB) * (BN * RB));
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < KS / 32; ++s) {
         bf16x8 af[NI], bfr[NJ];
 #pragma unroll
         for (int i = 0; i < NI; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(halo + ig_off(prow[i] + shift, 4 * s + fq));
+          af[i] = *reinterpret_cast<const bf16x8*>(halo + ha_off<KS>(prow[i] + shift, 4 * s + fq));
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ig_off(16 * j + fr, 4 * s + fq));
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ha_off<KS>(16 * j + fr, 4 * s + fq));
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -1458,7 +1474,8 @@ bool halo_ok(const GemmGeom& g) {
          g.pt == 1 && g.ph == 1 && g.pw == 1 && g.sT == g.dT && g.sH == g.dH && g.sW == g.dW &&
          g.dW % kHoW == 0;
 }
-// VDIFF_CONV_HALO: 0 never, 1 every eligible conv, 2 (default) where it measured faster.
+// VDIFF_CONV_HALO: 0 never, 1 every eligible conv, 2 (default) where it measured faster
+// (halo_ks below; the list that follows is the 64-channel-step measurement).
 // Same-box per-shape A/B over the config-2 train step (profiles/r02_ab_conv_halo.txt): the
 // halo tile wins for N <= 64 (fwd 200->64 / 192->64 0.66x, 64->64 0.87x, bwd-data 64->64
 // 0.84x) and at the 32x32 level up to N = 256 (0.68-0.83x); with N >= 128 at 64x64 and
@@ -1470,17 +1487,31 @@ std::atomic<int> g_halo_mode{[] {
   return e ? atoi(e) : 2;
 }()};
 int conv_halo_mode() { return g_halo_mode.load(std::memory_order_relaxed); }
-bool halo_use(const GemmGeom& g) {
+// Channels per halo step for this conv, 0 = the gathered-tile kernel.  64-channel steps (two
+// workgroups per CU) win at the 32x32 level, 32-channel steps (four per CU) on the larger
+// levels; per-shape A/B in profiles/r02_ab_conv_halo_ks.txt.  N = output channels of the
+// GEMM (Co fwd, Ci bwd-data), sC = its reduction channels.
+int halo_ks(const GemmGeom& g, bool tr) {
   const int m = conv_halo_mode();
-  if (m == 0 || !halo_ok(g)) return false;
-  return m == 1 || g.N <= 64 || (g.dW <= 32 && g.N <= 256);
+  if (m == 0 || !halo_ok(g)) return 0;
+  static const int force = [] {
+    const char* e = getenv("VDIFF_CONV_HALO_KS");
+    return e ? atoi(e) : 0;
+  }();
+  const int natural = g.dW <= 32 ? 64 : 32;
+  if (m == 1) return force ? force : natural;
+  int ks = 0;
+  if (g.dW <= 32) ks = g.N <= 256 ? 64 : 0;
+  else if (!tr) ks = g.N <= 128 ? 32 : 0;
+  else ks = g.sC <= 64 ? 32 : (g.N <= 64 ? 64 : 0);
+  return ks && force ? force : ks;
 }
-template <bool TR, int NSTB, int NW>
+template <bool TR, int NSTB, int NW, int KS = 64>
 void launch_halo_st(const GemmGeom& g, const void* src, const void* wt, void* dst,
                     const float* bias, const float* ca, const void* res, hipStream_t st) {
   const size_t lds_c = (size_t)128 * (64 + 4) * 4;
-  const size_t lds = halo_lds<NSTB>() > lds_c ? halo_lds<NSTB>() : lds_c;
-  auto kern = halo_conv_kernel<TR, NSTB, NW>;
+  const size_t lds = halo_lds<NSTB, KS>() > lds_c ? halo_lds<NSTB, KS>() : lds_c;
+  auto kern = halo_conv_kernel<TR, NSTB, NW, KS>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int64_t tiles = (int64_t)g.B * vd_cdiv(g.dT, kHoT) * vd_cdiv(g.dH, kHoH) * (g.dW / kHoW);
@@ -1503,9 +1534,13 @@ int conv_halo_stages() {
   return v;
 }
 template <bool TR>
-void launch_halo(const GemmGeom& g, const void* src, const void* wt, void* dst, const float* bias,
-                 const float* ca, const void* res, hipStream_t st) {
+void launch_halo(const GemmGeom& g, int ks, const void* src, const void* wt, void* dst,
+                 const float* bias, const float* ca, const void* res, hipStream_t st) {
   const int ns = conv_halo_stages();
+  if (ks == 32) {
+    launch_halo_st<TR, 3, 4, 32>(g, src, wt, dst, bias, ca, res, st);
+    return;
+  }
   if (conv_halo_waves() == 8) {
     if (ns == 5) launch_halo_st<TR, 5, 8>(g, src, wt, dst, bias, ca, res, st);
     else launch_halo_st<TR, 3, 8>(g, src, wt, dst, bias, ca, res, st);
@@ -1772,8 +1807,8 @@ int launch_gemm(const GemmGeom& g, const void* src, const void* wt, void* dst, c
     if (!g_legacy_conv && g_conv_dma && g.kt * g.kh * g.kw <= 32 && (!TR || unit) &&
         (int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2 < ((int64_t)1 << 31) &&
         (int64_t)g.N * g.K * 2 < ((int64_t)1 << 31)) {
-      if (halo_use(g)) {
-        launch_halo<TR>(g, src, wt, dst, bias, ca, res, st);
+      if (const int ks = halo_ks(g, TR)) {
+        launch_halo<TR>(g, ks, src, wt, dst, bias, ca, res, st);
         return VD_OK;
       }
       return launch_igemm_dma<TR>(g, src, wt, dst, bias, ca, res, st);
