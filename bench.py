@@ -2,8 +2,11 @@
 """Benchmark: train-step frames/sec + DDIM steps/sec, 128x128x16 UNet3D (BASELINE.json).
 
     python bench.py --gpus N --steps K --warmup W
-    (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
-             --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+    N > 1 without a launcher: the process starts `python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py ...`
+    itself (before anything touches the GPU) and exits with its status; under an external
+    launcher WORLD_SIZE must equal --gpus.  VDIFF_DIST_BACKEND=gloo rehearses N ranks on
+    fewer GPUs (ranks share GPUs round-robin).
 
 Workload (BASELINE config 2/3): the audio + reference-image conditioned UNet3D of
 train.py:88-97 with dims=3 (model_channels 64, mult (1,2,4), 2 res blocks,
@@ -74,8 +77,9 @@ def parse():
     ap.add_argument("--vivit-batch", type=int, default=16, help="clips per GPU (reference: 16)")
     ap.add_argument("--vivit-eager", action="store_true",
                     help="no HIP-graph capture of the ViViT step")
-    ap.add_argument("--vivit-graph-ddp", action="store_true",
-                    help="N > 1: graph-captured ViViT step around one all-reduce")
+    ap.add_argument("--vivit-eager-ddp", action="store_true",
+                    help="N > 1: eager ViViT step with the bucketed all-reduce instead of the "
+                         "graph replays around one all-reduce")
     ap.add_argument("--xattn-steps", type=int, default=3,
                     help="timed train steps with audio cross-attention (build extension, "
                          "auxiliary leg); 0 skips it")
@@ -310,10 +314,10 @@ def vivit_leg(args, rank, world, device):
     torch.manual_seed(4321)
     model = ViViT(VivitModel(cfg, use_bf16=args.dtype == "bf16"), 40, 5).to(device)
     broadcast_parameters(model)
-    # one process: the whole step as one HIP graph.  N > 1: eager with the bucketed
-    # all-reduce (the path the UNet leg proves at scale) unless --vivit-graph-ddp (graph
-    # replays around one all-reduce; rehearsed over gloo only)
-    graph = not args.vivit_eager and (world == 1 or args.vivit_graph_ddp)
+    # one process: the whole step as one HIP graph.  N > 1: forward + backward graph, ONE
+    # all-reduce of the flattened gradients, AdamW graph (VivitTrainer); --vivit-eager-ddp
+    # runs eager with the bucketed all-reduce instead
+    graph = not args.vivit_eager and (world == 1 or not args.vivit_eager_ddp)
     tr = VivitTrainer(model, graph=graph)
     g = torch.Generator(device=device).manual_seed(300 + rank)
     B = args.vivit_batch
@@ -384,8 +388,48 @@ def xattn_leg(args, rank, world, device, base_ms):
     return out
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """One process per GPU without an external launcher: run this same command line under
+    torch.distributed.run (N local ranks, rendezvous on 127.0.0.1) as a CHILD process and
+    return its exit status.  Called before anything in this process touches the GPU."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"spawning {n} ranks: {' '.join(cmd)}")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def comm_report(trainer, world, device, steps):
+    """Gradient exchange of the timed steps: bytes, RCCL world size, the exposed all-reduce
+    time per step (end of backward -> averaged buckets, max over ranks), the same exchange
+    issued alone, and the fraction of it hidden under the backward."""
+    bk = trainer.bucketer
+    exposed = bk.comm_times_ms()
+    exp_ms = max_over_ranks(sum(exposed) / max(len(exposed), 1), world, device)
+    alone = max_over_ranks(bk.standalone_allreduce_ms(), world, device)
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+            "grad_mbytes": round(bk.nbytes / 2 ** 20, 1), "buckets": len(bk.buckets),
+            "exposed_ms_per_step": round(exp_ms, 3), "standalone_ms_per_step": round(alone, 3),
+            "hidden_frac": round(1.0 - exp_ms / alone, 3) if alone > 0 else None,
+            "steps": len(exposed)}
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     from vdiff import ops
     from vdiff.ddp import broadcast_parameters, init_from_env
     from vdiff.engine import Trainer, synthetic_clip
@@ -394,7 +438,11 @@ def main():
 
     rank, world, local = init_from_env()
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE {world}")
+        sys.exit(2)
+    if world > 1 and dist.get_world_size() != world:
+        log(f"error: process group size {dist.get_world_size()} != WORLD_SIZE {world}")
+        sys.exit(2)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     torch.manual_seed(1234 + rank)
@@ -425,12 +473,18 @@ def main():
         barrier_sync(world)
         timer = ops.KernelTimer()
         ops.set_timer(timer)
+        if trainer.bucketer is not None:
+            trainer.bucketer.timing = True
         t0 = time.perf_counter()
         for _ in range(args.steps):
             loss = trainer.step(clip)
         barrier_sync(world)
         el = time.perf_counter() - t0
         ops.set_timer(None)
+        if trainer.bucketer is not None:
+            trainer.bucketer.timing = False
+            result["allreduce"] = comm_report(trainer, world, device, args.steps)
+            log("allreduce", result["allreduce"])
         el = max_over_ranks(el, world, device)
         ms = el / args.steps * 1e3
         result["value"] = round(world * frames_per_gpu * args.steps / el, 4)

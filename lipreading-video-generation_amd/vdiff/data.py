@@ -181,21 +181,33 @@ def audio_window(wave: np.ndarray, sr: int, fps: float, out_frame: int, buffer_f
     return out
 
 
+def _device_error(e: BaseException) -> bool:
+    """A HIP/CUDA initialisation or launch failure: never swallowed into (None, None) (a
+    forked DataLoader worker cannot re-initialise the GPU; hiding that only moves the error
+    to collate)."""
+    msg = str(e)
+    return isinstance(e, RuntimeError) and any(k in msg for k in ("CUDA", "HIP", "hip", "cuda"))
+
+
 class TalkingFaceFrameDataset(torch.utils.data.Dataset):
-    """dataset.py:68-139 over .vdclip files: (input_frame [3, S, S], output_frame [3, S, S],
-    {"input_values": [C, 4000]}); on any error it prints and returns (None, None) like the
-    reference.  `frame_transforms`, when given, is applied on the host to the uint8 frames
-    (the reference's torchvision Compose); otherwise the GPU transform runs on `device`.
+    """dataset.py:68-139 over .vdclip files: (input_frame, output_frame,
+    {"input_values": [C, 4000]}); on a data error it prints and returns (None, None) like the
+    reference.  Frames are what the reference returns: the raw uint8 [H, W, 3] frames when
+    `frame_transforms` is None, else frame_transforms(frame) (the reference's torchvision
+    Compose, on the host).  gpu_transform=True (opt-in, main process only) instead runs
+    ToPILImage -> Resize -> ToTensor -> Normalize on `device` (vd_frames_resize_normalize)
+    and returns [3, S, S] tensors there; device errors are raised, not swallowed.
     bug_compatible: reproduce process_audio's resample from orig_freq = channel count
     (dataset.py:53); False resamples from the track's rate (identity at 16 kHz)."""
 
     def __init__(self, frame_items, frame_transforms=None, frame_rate=30, audio_transforms=None,
-                 *, image_size=128, device="cuda", bug_compatible=True):
+                 *, image_size=128, gpu_transform=False, device="cuda", bug_compatible=True):
         self.frame_items = frame_items
         self.frame_transforms = frame_transforms
         self.frame_rate = frame_rate
         self.audio_transforms = audio_transforms
         self.image_size = image_size
+        self.gpu_transform = gpu_transform
         self.device = device
         self.bug_compatible = bug_compatible
 
@@ -210,17 +222,21 @@ class TalkingFaceFrameDataset(torch.utils.data.Dataset):
                 raise ValueError("FPS is zero, which may indicate an issue with the video file")
             out_idx = min(it.frame_end, len(c) - 1)
             pair = np.stack([c.frames[0], c.frames[out_idx]])  # input_frame_idx = 0 (:98)
-            if self.frame_transforms is not None:
-                inp, outp = self.frame_transforms(pair[0]), self.frame_transforms(pair[1])
-            else:
+            if self.gpu_transform:
                 f = transform_frames(torch.from_numpy(pair).to(self.device), self.image_size)
                 inp, outp = f[0], f[1]
+            elif self.frame_transforms is not None:
+                inp, outp = self.frame_transforms(pair[0]), self.frame_transforms(pair[1])
+            else:
+                inp, outp = pair[0], pair[1]
             a = audio_window(c.audio, c.sr, c.fps, out_idx, bug_compatible=self.bug_compatible)
             a = torch.from_numpy(a)
             if self.audio_transforms is not None:
                 a = self.audio_transforms(a)
             return inp, outp, {"input_values": a}
         except Exception as e:  # the reference's contract (dataset.py:137-139)
+            if _device_error(e):
+                raise
             print(f"Error processing video {it.video_path}: {e}")
             return None, None
 
@@ -231,16 +247,30 @@ class _Sample:
     out_idx: list
 
 
+@dataclass
+class _HostBatch:
+    frames: torch.Tensor | None   # pinned uint8 [B*(T+1), H, W, 3] (one frame size), or None
+    per_clip: list | None         # [uint8 [T+1, H, W, 3]] when the frame sizes differ
+    audio: torch.Tensor           # pinned fp32 [B*T, 4000]
+
+
 class ClipBatcher:
     """Training batches for the frame-stack denoiser from a frame index: per item the
     conditioning image is frame 0, the targets are `frames` consecutive output frames from
     min(frame_end, F - 1) on (stepping like the index, clipped to the last frame), each with
     its own audio window (frames = 1 is the reference's per-frame sample).
-    Frames go to the GPU once per batch (uint8, pinned) and through the resize kernel; eps
-    and t are drawn on the device.  Returns vdiff.engine.Clip."""
+
+    The host half of a batch (item draws, memory-mapped frame reads, the audio-window DSP,
+    pinned staging) runs on a background thread `prefetch` batches ahead -- the reference's
+    DataLoader(num_workers=4) (train.py:82) in one process, with no GPU context in a
+    worker.  The libvdiff DSP releases the GIL (ctypes), so it overlaps the host's kernel
+    launches.  next() takes the prepared batch, uploads it on the current stream (pinned,
+    asynchronous) and runs the resize kernel; eps and t are drawn on the device.  Draws are
+    sequential on one thread, so batches are the same as prefetch=0.  Returns
+    vdiff.engine.Clip."""
 
     def __init__(self, items, batch, frames, num_timesteps, device, size=128, seed=0,
-                 bug_compatible=True, dims=3):
+                 bug_compatible=True, dims=3, prefetch=2):
         self.items, self.batch, self.frames, self.size = list(items), batch, frames, size
         self.num_timesteps, self.device, self.dims = num_timesteps, device, dims
         self.bug_compatible = bug_compatible
@@ -248,6 +278,12 @@ class ClipBatcher:
         self.gen = torch.Generator(device=device).manual_seed(seed)
         if not self.items:
             raise ValueError("empty frame index")
+        self.prefetch = int(prefetch)
+        self._pool = None
+        self._pending = []
+        if self.prefetch > 0:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="vdclip")
 
     def _sample(self, it):
         c = open_clip(it.video_path)
@@ -255,36 +291,61 @@ class ClipBatcher:
         o = min(it.frame_end, len(c) - 1)
         return _Sample(c, [min(o + k * step, len(c) - 1) for k in range(self.frames)])
 
-    def next(self):
-        from .engine import Clip
-        B, T, S = self.batch, self.frames, self.size
+    def _host_batch(self) -> _HostBatch:
+        B = self.batch
         picks = [self._sample(self.items[i])
                  for i in self.rng.integers(0, len(self.items), size=B)]
-        shapes = {p.clip.frames.shape[1:] for p in picks}
+        stacks = [np.stack([p.clip.frames[0]] + [p.clip.frames[i] for i in p.out_idx])
+                  for p in picks]
+        audio = [audio_window(p.clip.audio, p.clip.sr, p.clip.fps, i,
+                              bug_compatible=self.bug_compatible)[0]  # mono: channel 0
+                 for p in picks for i in p.out_idx]
+        pin = torch.cuda.is_available()
+        audio = torch.from_numpy(np.stack(audio))
+        audio = audio.pin_memory() if pin else audio
+        if len({s.shape for s in stacks}) == 1:  # one upload and two launches for the batch
+            fr = torch.from_numpy(np.concatenate(stacks))
+            return _HostBatch(fr.pin_memory() if pin else fr, None, audio)
+        return _HostBatch(None, [torch.from_numpy(s) for s in stacks], audio)
+
+    def _fill(self):
+        while len(self._pending) < self.prefetch:
+            self._pending.append(self._pool.submit(self._host_batch))
+
+    def next(self):
+        from .engine import Clip
+        if self._pool is None:
+            hb = self._host_batch()
+        else:
+            self._fill()
+            hb = self._pending.pop(0).result()
+            self._fill()  # the next batch's host work starts now, beside this step
+        B, T, S = self.batch, self.frames, self.size
         x0 = torch.empty((B, T, 3, S, S), device=self.device)
         cond = torch.empty((B, 3, S, S), device=self.device)
-        audio = []
-        if len(shapes) == 1:  # one upload and two launches for the whole batch
-            host = torch.from_numpy(np.stack([np.stack([p.clip.frames[0]] +
-                                                       [p.clip.frames[i] for i in p.out_idx])
-                                              for p in picks])).pin_memory()
-            dev = host.to(self.device, non_blocking=True).reshape(B * (T + 1), *host.shape[2:])
+        if hb.frames is not None:
+            dev = hb.frames.to(self.device, non_blocking=True)
             f = transform_frames(dev, S).reshape(B, T + 1, 3, S, S)
             cond.copy_(f[:, 0])
             x0.copy_(f[:, 1:])
         else:
-            for b, p in enumerate(picks):
-                fr = torch.from_numpy(np.stack([p.clip.frames[0]] +
-                                               [p.clip.frames[i] for i in p.out_idx]))
+            for b, fr in enumerate(hb.per_clip):
                 f = transform_frames(fr.to(self.device), S)
                 cond[b], x0[b] = f[0], f[1:]
-        for p in picks:
-            for i in p.out_idx:
-                a = audio_window(p.clip.audio, p.clip.sr, p.clip.fps, i,
-                                 bug_compatible=self.bug_compatible)
-                audio.append(a[0])  # mono: channel 0 (the reference's [1, 4000])
-        audio = torch.from_numpy(np.stack(audio)).pin_memory().to(self.device, non_blocking=True)
+        audio = hb.audio.to(self.device, non_blocking=True)
         x0 = x0.transpose(1, 2).contiguous() if self.dims == 3 else x0[:, 0].contiguous()
         eps = torch.randn(x0.shape, generator=self.gen, device=self.device)
         t = torch.randint(0, self.num_timesteps, (B,), generator=self.gen, device=self.device)
         return Clip(x0, cond, {"input_values": audio}, eps, t)
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+            self._pending = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -67,9 +67,16 @@ class Trainer:
 
     train.py:102-103: Adam(model.parameters(), lr=1e-2), MSELoss."""
 
-    def __init__(self, model, scheduler, lr=1e-2, bucket_mb=25.0, fused_adam=True):
+    def __init__(self, model, scheduler, lr=1e-2, bucket_mb=25.0, fused_adam=True,
+                 check_every=50):
+        """check_every: the loss finiteness flag (kept on the device, updated every step) is
+        read on the host every `check_every` steps and by check_finite(); a non-finite
+        loss raises FloatingPointError naming the first bad step.  0 disables it."""
         self.model = model
         self.scheduler = scheduler
+        self.check_every = int(check_every)
+        self.steps_done = 0
+        self._first_bad = None  # device int64: first step with a non-finite loss, or -1
         params = [p for p in model.parameters() if p.requires_grad]
         # one process: no all-reduce, so no bucket views -- autograd hands each gradient over
         # without the accumulate-into-view add, and zero_grad drops them (no fills)
@@ -86,12 +93,36 @@ class Trainer:
         loss.backward()
         if self.bucketer is not None:
             self.bucketer.finish()
-        self.opt.step()
-        if self.bucketer is not None:
+            self.bucketer.step(self.opt)
             self.bucketer.zero_grad()
         else:
+            self.opt.step()
             self.opt.zero_grad(set_to_none=True)
-        return loss.detach()
+        loss = loss.detach()
+        self._track_finite(loss)
+        return loss
+
+    def _track_finite(self, loss):
+        """SURVEY 5 failure detection without a per-step host sync: a device-side record of
+        the first step whose loss is NaN/Inf (the reference skips nothing and checks
+        nothing, train.py:111-112), read every check_every steps."""
+        if self.check_every <= 0:
+            return
+        if self._first_bad is None:
+            self._first_bad = torch.full((), -1, dtype=torch.int64, device=loss.device)
+        bad = ~torch.isfinite(loss) & (self._first_bad < 0)
+        self._first_bad.copy_(torch.where(bad, self.steps_done, self._first_bad))
+        self.steps_done += 1
+        if self.steps_done % self.check_every == 0:
+            self.check_finite()
+
+    def check_finite(self):
+        """Raise FloatingPointError if any step so far had a non-finite loss (host sync)."""
+        if self._first_bad is not None:
+            first = int(self._first_bad)
+            if first >= 0:
+                raise FloatingPointError(f"non-finite training loss at step {first} "
+                                         f"(of {self.steps_done})")
 
 
 @torch.no_grad()
@@ -170,8 +201,8 @@ def _sample_ddim(model, sampler, cond, audio, shape, generator, callback):
         g = DDIMGraph(model, sampler, cond, feats, xt)
         for i in range(sampler.steps):
             xt, x0 = g.step(i)
-            if callback is not None:
-                callback(i, xt, x0)
+            if callback is not None:  # the graph's static buffers: the next replay rewrites them
+                callback(i, xt.clone(), x0.clone())
         return xt.clone(), x0.clone()
     for i in range(sampler.steps):
         t = torch.full((shape[0],), int(sampler.timesteps[i]), dtype=torch.int64, device=device)

@@ -292,14 +292,19 @@ class EmbTable:
 
 
 def emb_table(model, emb):
-    """EmbTable over the model's ResBlocks (cached list), or `emb` itself when the blocks
-    do not all share the reference emb_layers structure."""
-    blocks = getattr(model, "_resblocks", None)
-    if blocks is None:
+    """EmbTable over the model's ResBlocks, or `emb` itself when the blocks do not all share
+    the reference emb_layers structure.  The block list is cached together with the identity
+    of the module that built it: nn.DataParallel replicas (test.py:101) copy __dict__
+    shallowly, so a replica sees the original's cache under a different owner and rebuilds
+    it from its own (per-device) blocks."""
+    cached = model.__dict__.get("_resblocks")
+    if cached is None or cached[0] != id(model):
         blocks = [m for m in model.modules() if isinstance(m, ResBlock)]
         ok = all(isinstance(rb.emb_layers[0], SiLU) and isinstance(rb.emb_layers[1], nn.Linear)
                  for rb in blocks)
-        model._resblocks = blocks = blocks if ok else []
+        cached = (id(model), blocks if ok else [])
+        model.__dict__["_resblocks"] = cached
+    blocks = cached[1]
     return EmbTable(emb, blocks) if blocks else emb
 
 

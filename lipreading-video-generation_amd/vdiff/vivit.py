@@ -347,10 +347,11 @@ class VivitTrainer:
         loss.backward()
         if self.bucketer is not None:
             self.bucketer.finish()
-        self.opt.step()
-        if self.bucketer is not None:
+            self.bucketer.step(self.opt)
             self.bucketer.zero_grad()
-        elif zero:
+            return loss.detach()
+        self.opt.step()
+        if zero:
             self.opt.zero_grad(set_to_none=True)
         return loss.detach()
 

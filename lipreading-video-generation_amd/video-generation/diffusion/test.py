@@ -91,13 +91,16 @@ def load_model_and_scheduler(config, *, seed=0):
 
 
 def save_frame(x0, path):
-    """x0 in [-1, 1] -> (x0 + 1) / 2 as .npy and, for the first frame, .png (test.py:71-81)."""
+    """x0 in [-1, 1] -> (x0 + 1) / 2 as .npy and, for the first frame, .png (test.py:71-81).
+    The PNG quantises as transforms.ToPILImage does (mul(255) then truncation to uint8); the
+    clamp to [-1, 1] is a documented difference (the reference lets out-of-range values wrap
+    in .byte())."""
     ims = ((x0.float().clamp(-1, 1) + 1) / 2).cpu().numpy()
     np.save(path + ".npy", ims)
     try:
         from PIL import Image
         img = ims[0] if ims.ndim == 4 else ims[0][:, 0]
-        Image.fromarray((img.transpose(1, 2, 0) * 255).round().astype(np.uint8)).save(path + ".png")
+        Image.fromarray((img.transpose(1, 2, 0) * 255).astype(np.uint8)).save(path + ".png")
     except ImportError:
         pass
 

@@ -132,6 +132,7 @@ def train(argv=None):
                                       args.num_timesteps, device,
                                       seed=(epoch * 1000003 + step) * world + rank, dims=args.dims)
             loss = trainer.step(clip)
+        trainer.check_finite()  # the device-side NaN/Inf record, read once per epoch
         if rank == 0:
             dt = time.time() - t0
             fps = world * args.batch_size * frames * args.steps_per_epoch / dt

@@ -102,3 +102,24 @@ def test_clip_store_and_frame_index(tmp_path):
     bad = tmp_path / "bad.vdclip"
     bad.write_bytes(b"nope" * 20)
     assert vd.build_frame_items([str(bad)]) == []
+
+
+def test_dataset_returns_raw_frames_without_transforms(tmp_path):
+    """frame_transforms=None returns the raw uint8 frames, as the reference does (dataset.py:
+    105-107), with no GPU call (usable from DataLoader workers); a host transform is applied
+    per frame; data errors give (None, None) (dataset.py:137-139).  CPU."""
+    frames = np.random.default_rng(8).integers(0, 256, (12, 20, 24, 3), dtype=np.uint8)
+    p = str(tmp_path / "r.vdclip")
+    vd.write_clip(p, frames, 30.0, _wave(1, 8000, 16000, 9), 16000)
+    items = vd.build_frame_items([p])
+    ds = vd.TalkingFaceFrameDataset(items)
+    inp, outp, aud = ds[3]
+    out_idx = min(items[3].frame_end, 11)
+    assert inp.dtype == np.uint8 and inp.shape == (20, 24, 3)
+    np.testing.assert_array_equal(inp, frames[0])
+    np.testing.assert_array_equal(outp, frames[out_idx])
+    assert tuple(aud["input_values"].shape) == (1, 4000)
+    ds2 = vd.TalkingFaceFrameDataset(items, frame_transforms=lambda f: f[::2, ::2].copy())
+    np.testing.assert_array_equal(ds2[3][1], frames[out_idx][::2, ::2])
+    assert vd.TalkingFaceFrameDataset([vd.FrameItem(str(tmp_path / "no.vdclip"), 0, 1)])[0] \
+        == (None, None)

@@ -147,6 +147,9 @@ def test_bucket_order_survives_rank_dependent_unused_params():
         torch.testing.assert_close(g, sum(gr[i] for gr in grads) / world, atol=1e-6, rtol=1e-5)
 
 
+_GSKIPS = {0: (1, 2), 1: (2,)}  # block 2 unused on every rank, block 1 on rank 0 only
+
+
 def _global_skip_worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -154,27 +157,33 @@ def _global_skip_worker(rank, world, port, out):
     init_from_env("gloo")
     m = _Skippy()
     bk = GradBucketer(list(m.parameters()), bucket_mb=0.003)
-    skips = {0: (1, 2), 1: (2,)}  # block 2 unused on every rank, block 1 on rank 0 only
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-2, weight_decay=0.1)
     x, y = _data()
     n = x.shape[0] // world
-    state = []
-    for step in range(2):
-        loss = torch.nn.functional.mse_loss(m(x[rank * n:(rank + 1) * n], skips[rank]),
+    unused = []
+    for step in range(3):
+        loss = torch.nn.functional.mse_loss(m(x[rank * n:(rank + 1) * n], _GSKIPS[rank]),
                                             y[rank * n:(rank + 1) * n])
         loss.backward()
         bk.finish()
-        state.append([p.grad is None for p in m.parameters()])
+        names = {id(p): k for k, p in m.named_parameters()}
+        unused.append(sorted(names[id(bk.views[i][0])] for i in bk.globally_unused()))
+        bk.step(opt)
         bk.zero_grad()
     if rank == 0:
-        out.put(state + [[p.grad is None for p in m.parameters()]])
+        out.put({"params": [p.detach().numpy().copy() for p in m.parameters()],
+                 "unused": unused,
+                 "grads_are_views": all(p.grad is not None for p in m.parameters())})
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_globally_unused_params_get_no_grad():
-    """A parameter no rank produced a gradient for gets .grad = None for the optimizer step
-    (as in one process: AdamW's weight decay must not touch it); zero_grad() re-arms the
-    bucket views.  A parameter unused on one rank only keeps its (averaged) gradient."""
+def test_globally_unused_params_keep_weights_and_state():
+    """A parameter no rank produced a gradient for is left alone by the optimizer step (as
+    with .grad = None in one process: AdamW's weight decay and moments must not touch it),
+    decided on the device from the used-flags carried by the last bucket -- no host sync.
+    A parameter unused on one rank only is updated with its averaged gradient.  The result
+    equals a single process that averages the ranks' gradients by hand."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -187,8 +196,27 @@ def test_globally_unused_params_get_no_grad():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    names = [n for n, _ in _Skippy().named_parameters()]
-    for step_state in got[:2]:
-        none = {n for n, is_none in zip(names, step_state) if is_none}
-        assert none == {"blocks.2.weight", "blocks.2.bias"}, none
-    assert not any(got[2])  # after zero_grad every parameter has its bucket view again
+    assert got["unused"] == [["blocks.2.bias", "blocks.2.weight"]] * 3
+    assert got["grads_are_views"]
+    m = _Skippy()
+    init = {k: v.detach().clone() for k, v in m.named_parameters()}
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-2, weight_decay=0.1)
+    x, y = _data()
+    n = x.shape[0] // world
+    for _ in range(3):
+        per_rank = []
+        for r in range(world):
+            m.zero_grad(set_to_none=True)
+            torch.nn.functional.mse_loss(m(x[r * n:(r + 1) * n], _GSKIPS[r]),
+                                         y[r * n:(r + 1) * n]).backward()
+            per_rank.append([None if p.grad is None else p.grad.clone() for p in m.parameters()])
+        for i, p in enumerate(m.parameters()):
+            gs = [g[i] for g in per_rank]
+            p.grad = (None if all(g is None for g in gs) else
+                      sum(g if g is not None else torch.zeros_like(p) for g in gs) / world)
+        opt.step()
+    for (name, p), g in zip(m.named_parameters(), got["params"]):
+        g = torch.from_numpy(g)
+        torch.testing.assert_close(g, p.detach(), atol=1e-6, rtol=1e-5)
+        if name.startswith("blocks.2."):
+            torch.testing.assert_close(g, init[name], atol=0, rtol=0)

@@ -53,7 +53,7 @@ def test_dataset_item_matches_oracle(tmp_path):
     from vdiff import data as vd
     p = _store(tmp_path, "v0", seed=3)
     items = vd.build_frame_items([p])
-    ds = vd.TalkingFaceFrameDataset(items, device=dev)
+    ds = vd.TalkingFaceFrameDataset(items, gpu_transform=True, device=dev)
     c = vd.ClipFile(p)
     for idx in (0, 7, len(items) - 1):
         inp, outp, aud = ds[idx]
@@ -90,6 +90,26 @@ def test_clip_batcher_frame_stacks(tmp_path):
         for k, fi in enumerate(s.out_idx):
             np.testing.assert_array_equal(clip.x0[bi, :, k].cpu().numpy(),
                                           od.frame_transform(np.asarray(c.frames[fi]), 64))
+    b.close()
+
+
+def test_clip_batcher_prefetch_gives_the_same_batches(tmp_path):
+    """The background host thread (prefetch > 0) draws and prepares batches in order: the
+    batches equal the synchronous batcher's, frame for frame and window for window."""
+    from vdiff import data as vd
+    paths = [_store(tmp_path, f"v{i}", F=24, H=96 + 32 * (i % 2), W=96, seed=40 + i)
+             for i in range(3)]
+    items = vd.build_frame_items(paths)
+    got = {}
+    for pf in (0, 3):
+        b = vd.ClipBatcher(items, batch=2, frames=3, num_timesteps=100, device=dev, size=32,
+                           seed=11, prefetch=pf)
+        got[pf] = [b.next() for _ in range(5)]
+        b.close()
+    for a, c in zip(got[0], got[3]):
+        for k in ("x0", "cond", "eps", "t"):
+            assert torch.equal(getattr(a, k), getattr(c, k)), k
+        assert torch.equal(a.audio["input_values"], c.audio["input_values"])
 
 
 def test_train_entry_reads_a_frame_index(tmp_path):

@@ -30,11 +30,19 @@ def test_ddim_graph_matches_eager(dims, bf16, monkeypatch):
     cond = torch.rand((1, 3, 32, 32), device=dev) * 2 - 1
     feats = torch.randn((T, 64), device=dev)
     sampler = DDIMSampler(LinearNoiseSchedulerV2(500, 0.00005, 0.015), steps=5)
-    out = {}
+    out, traj = {}, {}
     for mode in ("0", "1"):
         monkeypatch.setenv("VDIFF_DDIM_GRAPH", mode)
         g = torch.Generator(device=dev).manual_seed(9)
-        out[mode] = sample_ddim(m, sampler, cond, feats, shape, generator=g)
+        seen = traj[mode] = []
+        out[mode] = sample_ddim(m, sampler, cond, feats, shape, generator=g,
+                                callback=lambda i, xt, x0: seen.append((xt, x0)))
     for a, b in zip(out["0"], out["1"]):
         assert torch.isfinite(a).all() and a.abs().max() > 0
         assert torch.equal(a, b)
+    # a callback that keeps references sees every step's own values on both paths (the
+    # graph path hands out copies of its static buffers, advisor r2)
+    assert len(traj["0"]) == len(traj["1"]) == 5
+    for (xa, x0a), (xb, x0b) in zip(traj["0"], traj["1"]):
+        assert torch.equal(xa, xb) and torch.equal(x0a, x0b)
+    assert not torch.equal(traj["1"][0][1], traj["1"][-1][1])
