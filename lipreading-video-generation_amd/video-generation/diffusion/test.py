@@ -115,25 +115,34 @@ def _frames_of(model, audio_cond):
 
 @torch.no_grad()
 def sample_images(model, scheduler, img_cond, audio_cond, n_timesteps=500, *, out_dir=OUT_DIR,
-                  save_every=50, generator=None):
+                  save_every=50, generator=None, noise=None, max_steps=None, callback=None):
     """test.py:51-83: reverse process i = n_timesteps-1 .. 0 with
     scheduler.sample_prev_timestep (LinearNoiseSchedulerV2 in test.py), x0 saved every
-    `save_every` steps and at i == 0; returns the final x0."""
+    `save_every` steps and at i == 0; returns the final x0.
+
+    Keyword-only extensions: `noise(shape)` supplies x_T and each step's z instead of
+    torch.randn (injected noise: the trajectory parity tests); `max_steps` stops after that
+    many steps; `callback(i, xt, x0)` sees every step's output."""
     model.eval()
     dev = img_cond.device
     S = config["dataset_params"]["im_size"]
     T = _frames_of(model, audio_cond)
     shape = (1, 3, S, S) if T is None else (1, 3, T, S, S)
     os.makedirs(out_dir, exist_ok=True)
+    draw = noise or (lambda shp: torch.randn(shp, generator=generator, device=dev))
     feats = model.encode_audio(audio_cond)  # once per clip (the reference: every step)
-    xt = torch.randn(shape, generator=generator, device=dev)
+    xt = draw(shape).to(dev)
     x0 = None
     with frozen_weights():  # packed conv weights reused across the steps
-        for i in reversed(range(n_timesteps)):
+        for k, i in enumerate(reversed(range(n_timesteps))):
+            if max_steps is not None and k == max_steps:
+                break
             t = torch.tensor([i], dtype=torch.long, device=dev)
             eps = model(xt, img_cond, feats, t)
-            z = torch.randn(xt.shape, generator=generator, device=dev)
+            z = draw(xt.shape).to(dev)
             xt, x0 = scheduler.sample_prev_timestep(xt, eps, t, z=z)
+            if callback is not None:
+                callback(i, xt, x0)
             if (i + 1) % save_every == 0 or i == 0:
                 save_frame(x0, os.path.join(out_dir, f"x0_{i}"))
     print("All images have been processed and saved.")

@@ -319,8 +319,100 @@ def gen_train_step():
     save("train_step_tiny3d.npz", **out)
 
 
+# ------------------------------------------------------------------ sampling trajectories
+TRAJ_STEPS = 10
+TRAJ_KEEP = (1, 5, 10)  # steps whose x_t / x0 are stored
+
+
+def _ref_trajectory(model_fn, shape, n_timesteps, steps, seed):
+    """The reference sampling loop (test.py:56-65, restated: test.py itself is a script that
+    needs torchvision and a checkpoint) over the imported LinearNoiseSchedulerV2(500, 5e-5,
+    0.015) (test.py:111).  The initial x_T (test.py:53) and every step's z (randn_like at
+    linear_noise_scheduler.py:97) are drawn as oracle.fixtures.seeded(shape, seed + k) and
+    injected by replacing torch.randn_like while the loop runs, so the test regenerates them
+    from the seeds."""
+    sched = ref_lns.LinearNoiseSchedulerV2(500, 0.00005, 0.015)
+    xt = seeded(shape, seed)
+    zs = iter(seeded(shape, seed + 1 + k) for k in range(steps))
+    orig = torch.randn_like
+    torch.randn_like = lambda x, *a, **k: next(zs)
+    out = {}
+    try:
+        with torch.no_grad():
+            for k, i in enumerate(reversed(range(n_timesteps))):
+                if k == steps:
+                    break
+                t = torch.tensor([i]).long()
+                eps = model_fn(xt, t).detach()
+                xt, x0 = sched.sample_prev_timestep(xt, eps, t)
+                if k + 1 in TRAJ_KEEP or k + 1 == steps:
+                    out[f"xt_{k + 1}"] = xt.clone()
+                    out[f"x0_{k + 1}"] = x0.clone()
+    finally:
+        torch.randn_like = orig
+    return out
+
+
+def gen_trajectory():
+    """Denoised frames over a sampling trajectory (north_star parity bar):
+    the first TRAJ_STEPS steps of a 500-step reverse process, and a whole n_timesteps = 10
+    call, on
+      * the tiny UNet3D (BASELINE config 1 shape, 64x64x8): conditioning restated around
+        the reference UNetModel as in gen_train_step (one reference image per clip, one
+        pooled audio window per frame);
+      * the full-width 2-D UNetModel at 64x64 (train.py's topology, the reference's literal
+        per-frame semantics): UNetAudio's conditioning (unet_audio.py:52-61) restated.
+    Audio enters as pooled wav2vec2 states (seeded), as in the other UNetAudio fixtures."""
+    out = {}
+    # tiny 3-D
+    m = ref_unet.UNetModel(image_size=64, **TINY3D)
+    m.eval()
+    load_init(m, 1234)
+    A = init_params(audio_param_shapes(64, 16, im_cond_output_ch=16), 77)
+    lin = nn.Linear(64, 16)
+    lin.weight.data.copy_(A["audio_transformer.transform.0.weight"])
+    lin.bias.data.copy_(A["audio_transformer.transform.0.bias"])
+    cc = nn.Conv2d(3, 16, 1, bias=False)
+    cc.weight.data.copy_(A["cond_conv_in.weight"])
+    T, S = 8, 64
+    cond = seeded((1, 3, 32, 32), 80, "uniform")
+    feat = seeded((T, 64), 81)
+
+    def tiny(xt, t):
+        a = F.relu(lin(feat)).reshape(1, T, 16).permute(0, 2, 1).reshape(1, 16, T, 1, 1)
+        a = a.expand(-1, -1, -1, S, S)
+        imc = cc(F.interpolate(cond, size=(S, S))).unsqueeze(2).expand(-1, -1, T, -1, -1)
+        return m(torch.cat([xt, imc, a], dim=1), t)
+
+    for k, v in _ref_trajectory(tiny, (1, 3, T, S, S), 500, TRAJ_STEPS, 900).items():
+        out["tiny3d_500_" + k] = v
+    # full-width 2-D at 64x64
+    m2 = ref_unet.UNetModel(image_size=64, **FULL2D)
+    m2.eval()
+    load_init(m2, 1234)
+    A2 = init_params(audio_param_shapes(768, 128), 77)
+    lin2 = nn.Linear(768, 128)
+    lin2.weight.data.copy_(A2["audio_transformer.transform.0.weight"])
+    lin2.bias.data.copy_(A2["audio_transformer.transform.0.bias"])
+    cc2 = nn.Conv2d(3, 64, 1, bias=False)
+    cc2.weight.data.copy_(A2["cond_conv_in.weight"])
+    cond2 = seeded((1, 3, 48, 48), 82, "uniform")
+    feat2 = seeded((1, 768), 83)
+
+    def full2d(xt, t):
+        af = F.relu(lin2(feat2)).view(-1, 128, 1, 1).expand(-1, -1, 64, 64)
+        imc = cc2(F.interpolate(cond2, size=xt.shape[-2:]))
+        return m2(torch.cat([xt, imc, af], dim=1), t)
+
+    for k, v in _ref_trajectory(full2d, (1, 3, 64, 64), 500, TRAJ_STEPS, 920).items():
+        out["full2d_500_" + k] = v
+    for k, v in _ref_trajectory(full2d, (1, 3, 64, 64), 10, 10, 940).items():
+        out["full2d_10_" + k] = v
+    save("trajectory.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["schedulers", "blocks", "models", "train_step"]
+    which = sys.argv[1:] or ["schedulers", "blocks", "models", "train_step", "trajectory"]
     if "schedulers" in which:
         gen_schedulers()
     if "blocks" in which:
@@ -329,3 +421,5 @@ if __name__ == "__main__":
         gen_models()
     if "train_step" in which:
         gen_train_step()
+    if "trajectory" in which:
+        gen_trajectory()
