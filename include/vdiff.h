@@ -250,11 +250,12 @@ size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d);
  * head_dim-64 forward with / without staggered wave halves, 7 the same with 4 waves and
  * two workgroups per CU, 8 the paired-wave head_dim-128 dK/dV, 9 the pipelined head_dim-64
  * backward with 4 waves x 2 blocks, 10 the role-split head_dim-256 dK/dV, 11 the
- * fragment-pipelined head_dim-64 backward (shapes a kernel does not take keep their
- * default).  Process-wide; returns the previous setting, or -2 for an invalid cfg
- * (vd_last_error says why).  Initial value from env VDIFF_ATTN_CFG
- * (base|nb2|w8|p8|p4|d8|d8n|d4|pair|p4n2|role|sp).  No reference counterpart: an A/B and
- * test hook. */
+ * fragment-pipelined head_dim-64 backward, 12 the hand-scheduled head_dim-64 dQ (one wave
+ * per SIMD, asm/gen_attn_asm.py) (shapes a kernel does not take keep their default).
+ * Process-wide; returns the previous setting, or -2 for an invalid cfg (vd_last_error says
+ * why).  Initial value from env VDIFF_ATTN_CFG
+ * (base|nb2|w8|p8|p4|d8|d8n|d4|pair|p4n2|role|sp|asm).  No reference counterpart: an A/B
+ * and test hook. */
 int vd_attention_set_config(int cfg);
 /* dout uses the o_* strides; dq/dk/dv use the q/k/v strides (so they can be
  * written straight into a d(qkv) buffer) and are OVERWRITTEN. */

@@ -1,0 +1,263 @@
+"""Small assembler-text toolkit for the hand-scheduled gfx950 kernels (attn_asm.s).
+
+The hot loops of the head_dim-64 attention kernels are emitted as explicit instruction
+streams: MFMAs in a fixed order, with the softmax VALU work and the LDS fragment reads
+placed into the gaps between them by position (MI355X_MICROARCH.md: per
+v_mfma_f32_32x32x16_bf16 gap one wave can hide about 24 cycles of vector issue).  This
+module provides
+  * `Regs`  -- named register ranges (VGPR / AGPR / SGPR);
+  * `Stream` -- an instruction list that tracks the wait-state hazards gfx950 does not
+    interlock and pads them with s_nop, and derives the counted lgkmcnt waits of every
+    consumer of an LDS read;
+  * `kernel_text` -- the code object wrapper (.amdhsa_kernel descriptor + metadata).
+
+Hazard distances (gfx950, measured from hipcc's own padding of the same instruction pairs):
+MFMA 32x32x16 write -> VALU / VMEM / DS / MFMA-A/B read 12 wait states; VALU write -> MFMA
+read 2; transcendental write -> VALU read 2 (one instruction between); an MFMA reading its
+own accumulator chain as srcC needs none.  Wait states are counted as issued instructions
+(s_nop n = n + 1), which under-counts the cycles an MFMA occupies, so the padding is
+conservative.
+"""
+from __future__ import annotations
+
+import re
+
+
+class Regs:
+    """Named register ranges in one file ('v', 'a' or 's')."""
+
+    def __init__(self, kind: str, start: int = 0):
+        self.kind, self.next, self.names = kind, start, {}
+
+    def alloc(self, name: str, n: int, align: int = 1) -> int:
+        if self.next % align:
+            self.next += align - self.next % align
+        base = self.next
+        self.names[name] = (base, n)
+        self.next += n
+        return base
+
+    def __getitem__(self, name):
+        return self.names[name][0]
+
+    def r(self, name, off=0, n=1) -> str:
+        b, size = self.names[name]
+        assert off + n <= size, (name, off, n, size)
+        return reg(self.kind, b + off, n)
+
+
+def reg(kind: str, i: int, n: int = 1) -> str:
+    return f"{kind}{i}" if n == 1 else f"{kind}[{i}:{i + n - 1}]"
+
+
+_RANGE = re.compile(r"\b([vas])\[(\d+):(\d+)\]|\b([vas])(\d+)\b")
+
+
+def regs_of(text: str) -> set:
+    """Physical registers named in an operand string: {('v', 12), ('a', 3), ...}."""
+    out = set()
+    for m in _RANGE.finditer(text):
+        if m.group(1):
+            k, lo, hi = m.group(1), int(m.group(2)), int(m.group(3))
+            out.update((k, i) for i in range(lo, hi + 1))
+        else:
+            out.add((m.group(4), int(m.group(5))))
+    return out
+
+
+def classify(op: str) -> str:
+    if op.startswith("v_mfma"):
+        return "mfma"
+    if op in ("v_exp_f32", "v_log_f32", "v_rcp_f32", "v_rsq_f32", "v_sqrt_f32"):
+        return "trans"
+    if op.startswith("v_"):
+        return "valu"
+    if op.startswith("ds_"):
+        return "ds"
+    if op.startswith(("buffer_", "global_")):
+        return "vmem"
+    return "salu"
+
+
+class Ins:
+    __slots__ = ("text", "op", "kind", "defs", "uses", "srcc", "lds_id", "wait_lds")
+
+    def __init__(self, text, lds_id=None, wait_lds=()):
+        self.text = text.strip()
+        self.op = self.text.split()[0]
+        self.kind = classify(self.op)
+        ops = self.text[len(self.op):].split(",")
+        ops = [o.strip() for o in ops]
+        self.srcc = set()
+        if self.kind in ("mfma", "trans", "valu"):
+            self.defs = regs_of(ops[0]) if ops and ops[0] else set()
+            self.uses = set().union(*[regs_of(o) for o in ops[1:]]) if len(ops) > 1 else set()
+            if self.kind == "mfma" and len(ops) >= 4:
+                self.srcc = regs_of(ops[3])
+        elif self.kind == "ds":
+            if self.op.startswith("ds_read"):
+                self.defs, self.uses = regs_of(ops[0]), regs_of(ops[1].split()[0])
+            else:
+                self.defs, self.uses = set(), set().union(*[regs_of(o.split()[0]) for o in ops])
+        elif self.kind == "vmem":
+            if "lds" in self.text.split() or self.op.startswith(("buffer_store", "global_store")):
+                self.defs, self.uses = set(), set().union(*[regs_of(o.split()[0]) for o in ops])
+            else:
+                self.defs = regs_of(ops[0])
+                self.uses = set().union(*[regs_of(o.split()[0]) for o in ops[1:]])
+        else:
+            self.defs, self.uses = set(), set()
+        self.lds_id = lds_id          # id of this LDS read (for counted waits)
+        self.wait_lds = tuple(wait_lds)  # LDS read ids this instruction consumes
+
+
+class Stream:
+    """Straight-line instruction stream with hazard padding and counted lgkmcnt waits.
+
+    Every ds_read must carry an lds_id; an instruction that consumes LDS-read results names
+    them in wait_lds and gets the weakest `s_waitcnt lgkmcnt(k)` that covers them (reads
+    complete in issue order).  Call `flush_lds()` to forget outstanding reads (after an
+    explicit lgkmcnt(0))."""
+
+    MFMA_RAW = 12      # MFMA write -> VALU / VMEM / DS / MFMA A-B read (and write)
+    VALU_TO_MFMA = 2   # VALU write -> MFMA read
+    TRANS_RAW = 2      # transcendental write -> VALU read
+    MFMA_WAR = 12      # VALU write of an in-flight MFMA's source
+
+    def __init__(self):
+        self.lines = []
+        self.hist = []        # (position, Ins) of the hazard-relevant recent instructions
+        self.pos = 0          # wait states issued so far
+        self.pending = []     # outstanding LDS read ids, issue order
+        self.nops = 0
+        self.waits = 0
+
+    def comment(self, text):
+        self.lines.append(f"\t; {text}")
+
+    def label(self, name):
+        self.lines.append(f"{name}:")
+
+    def raw(self, text, ws=1):
+        """An instruction outside the hazard model (branches, barriers, SALU)."""
+        self.lines.append("\t" + text)
+        self.pos += ws
+
+    def _need(self, ins: Ins) -> int:
+        need = 0
+        for p, h in reversed(self.hist):
+            d = self.pos - p
+            if d >= 13:
+                break
+            if h.kind == "mfma":
+                if ins.kind == "mfma":
+                    # chained accumulator (srcC == the producer's dst) needs no padding
+                    touched = (ins.uses - ins.srcc) & h.defs
+                    if touched:
+                        need = max(need, self.MFMA_RAW - d)
+                elif (ins.uses | ins.defs) & h.defs:
+                    need = max(need, self.MFMA_RAW - d)
+                if ins.kind in ("valu", "trans", "ds", "vmem") and ins.defs & (h.uses | h.srcc):
+                    need = max(need, self.MFMA_WAR - d)
+            elif h.kind in ("valu", "trans"):
+                if ins.kind == "mfma" and (ins.uses | ins.defs) & h.defs:
+                    need = max(need, self.VALU_TO_MFMA - d)
+                if h.kind == "trans" and ins.kind in ("valu", "trans", "vmem", "ds") \
+                        and ins.uses & h.defs:
+                    need = max(need, self.TRANS_RAW - d)
+        return need
+
+    def emit(self, text, lds_id=None, wait_lds=()):
+        ins = Ins(text, lds_id, wait_lds)
+        if ins.wait_lds:
+            idx = [self.pending.index(i) for i in ins.wait_lds if i in self.pending]
+            if idx:
+                k = len(self.pending) - 1 - max(idx)
+                self.lines.append(f"\ts_waitcnt lgkmcnt({min(k, 15)})")
+                self.pending = self.pending[max(idx) + 1:]
+                self.pos += 1
+                self.waits += 1
+        need = self._need(ins)
+        while need > 0:
+            n = min(need, 16)
+            self.lines.append(f"\ts_nop {n - 1}")
+            self.pos += n
+            self.nops += n
+            need -= n
+        self.lines.append("\t" + ins.text)
+        if ins.lds_id is not None:
+            self.pending.append(ins.lds_id)
+        if ins.kind in ("mfma", "valu", "trans"):
+            self.hist.append((self.pos, ins))
+            if len(self.hist) > 64:
+                self.hist = self.hist[-64:]
+        self.pos += 1
+        return ins
+
+    def flush_lds(self):
+        self.pending = []
+
+    def text(self):
+        return "\n".join(self.lines) + "\n"
+
+
+def kernel_text(name, body, *, vgprs, agprs, sgprs, lds_bytes, kernarg_bytes, wg_size,
+                wg_ids=(1, 1, 1)):
+    """A complete .s with one kernel (descriptor + HSA metadata, code object v5)."""
+    accum = (vgprs + 3) // 4 * 4
+    total = accum + agprs
+    assert total <= 512, total
+    return f""".amdgcn_target "amdgcn-amd-amdhsa--gfx950"
+.amdhsa_code_object_version 5
+.text
+.globl {name}
+.p2align 8
+.type {name},@function
+{name}:
+{body}
+\ts_endpgm
+.Lfunc_end_{name}:
+.size {name}, .Lfunc_end_{name}-{name}
+
+.rodata
+.p2align 6
+.amdhsa_kernel {name}
+  .amdhsa_group_segment_fixed_size {lds_bytes}
+  .amdhsa_private_segment_fixed_size 0
+  .amdhsa_kernarg_size {kernarg_bytes}
+  .amdhsa_user_sgpr_count 2
+  .amdhsa_user_sgpr_kernarg_segment_ptr 1
+  .amdhsa_system_sgpr_workgroup_id_x {wg_ids[0]}
+  .amdhsa_system_sgpr_workgroup_id_y {wg_ids[1]}
+  .amdhsa_system_sgpr_workgroup_id_z {wg_ids[2]}
+  .amdhsa_system_vgpr_workitem_id 0
+  .amdhsa_next_free_vgpr {total}
+  .amdhsa_next_free_sgpr {sgprs}
+  .amdhsa_accum_offset {accum}
+  .amdhsa_reserve_vcc 1
+  .amdhsa_float_denorm_mode_32 3
+  .amdhsa_float_denorm_mode_16_64 3
+  .amdhsa_ieee_mode 1
+  .amdhsa_dx10_clamp 1
+.end_amdhsa_kernel
+
+.amdgpu_metadata
+---
+amdhsa.version: [ 1, 2 ]
+amdhsa.kernels:
+  - .name: {name}
+    .symbol: {name}.kd
+    .kernarg_segment_size: {kernarg_bytes}
+    .group_segment_fixed_size: {lds_bytes}
+    .private_segment_fixed_size: 0
+    .kernarg_segment_align: 8
+    .wavefront_size: 64
+    .sgpr_count: {sgprs + 6}
+    .vgpr_count: {total}
+    .agpr_count: {agprs}
+    .max_flat_workgroup_size: {wg_size}
+    .args:
+      - {{ .offset: 0, .size: {kernarg_bytes}, .value_kind: by_value }}
+...
+.end_amdgpu_metadata
+"""

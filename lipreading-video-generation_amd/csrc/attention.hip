@@ -28,6 +28,7 @@
 // product, fp32 softmax and accumulation).  fp32 parity mode:
 // v_mfma_f32_32x32x2_f32 with the same structure (exact fp32 products).
 #include "vd_common.h"
+#include "vd_asm.h"
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -2496,7 +2497,7 @@ int check_attn(const vd_attn_desc* d) {
 //   kSP: the fragment-pipelined backward kernels (attn_bwd_dq_sp_kernel /
 //          attn_bwd_dkdv_sp_kernel; bf16, D = 64, >= 16 key tiles; fwd keeps its default)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
-               kPair = 8, kP4N2 = 9, kRole = 10, kSP = 11, kCfgLast = kSP };
+               kPair = 8, kP4N2 = 9, kRole = 10, kSP = 11, kAsm = 12, kCfgLast = kAsm };
 
 int cfg_from_env() {
   const char* e = getenv("VDIFF_ATTN_CFG");
@@ -2513,6 +2514,7 @@ int cfg_from_env() {
   if (!strcmp(e, "p4n2")) return (int)kP4N2;
   if (!strcmp(e, "role")) return (int)kRole;
   if (!strcmp(e, "sp")) return (int)kSP;
+  if (!strcmp(e, "asm")) return (int)kAsm;
   return -1;
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
@@ -2532,6 +2534,7 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
       !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
+      !(env == kAsm && (D != 64 || kind != 1)) &&    // hand-scheduled: D = 64 dQ
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
@@ -2798,6 +2801,47 @@ int dkdv_sp_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
 // sequences keep the 8-wave pipelines
 inline bool sp_ok(const vd_attn_desc* d) { return d->seq_len >= 16 * kTile; }
 
+// hand-scheduled head_dim-64 dQ (asm/gen_attn_asm.py): one wave per SIMD, 256 queries per
+// workgroup, tiles rounded up to the 4-stage ring; 32-bit buffer offsets of every row it
+// touches (the last DMA'd tiles run up to 5 tiles past the end), 16-B aligned rows
+inline bool asm_dq_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                      const void* dout, const void* dq) {
+  const int64_t n = d->seq_len;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return d->dtype == VD_BF16 && d->head_dim == 64 && n >= 16 * kTile && d->nseq % d->groups == 0 &&
+         d->token_stride % 8 == 0 && d->o_token_stride % 8 == 0 && d->token_stride >= 64 &&
+         d->o_token_stride >= 64 && d->batch_stride % 8 == 0 && d->group_stride % 8 == 0 &&
+         d->o_batch_stride % 8 == 0 && d->o_group_stride % 8 == 0 &&
+         (n + 512) * d->token_stride * 2 < 0x7fffffffLL &&
+         (n + 512) * d->o_token_stride * 2 < 0x7fffffffLL && al(q) && al(k) && al(v) &&
+         al(dout) && al(dq);
+}
+
+int dq_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                  const void* dout, const float* nlse2, const float* ndelta, void* dq,
+                  hipStream_t st) {
+  const int64_t n = d->seq_len;
+  vd::AsmDqArgs a{};
+  a.q = q; a.k = k; a.v = v; a.dout = dout; a.nlse2 = nlse2; a.ndelta = ndelta; a.dq = dq;
+  a.n = (uint32_t)n;
+  a.ts_bytes = (uint32_t)(d->token_stride * 2);
+  a.ots_bytes = (uint32_t)(d->o_token_stride * 2);
+  a.groups = (uint32_t)d->groups;
+  a.bs_bytes = (uint64_t)d->batch_stride * 2;
+  a.gs_bytes = (uint64_t)d->group_stride * 2;
+  a.obs_bytes = (uint64_t)d->o_batch_stride * 2;
+  a.ogs_bytes = (uint64_t)d->o_group_stride * 2;
+  a.scale = d->scale;
+  a.qscale = d->scale * kLog2e;  // the fp32 product RowFrag::scale receives
+  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 64) * 2);
+  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 64) * 2);
+  a.tile_bytes = (uint32_t)(kTile * d->token_stride * 2);
+  a.niter = (uint32_t)vd_cdiv(vd_cdiv(n, kTile), 4);
+  const int rc = vd::asm_bwd_dq_d64(a, (unsigned)vd_cdiv(n, 256), (unsigned)d->groups,
+                                    (unsigned)(d->nseq / d->groups), st);
+  return rc ? rc : vd::check_launch("attn_bwd_dq");
+}
+
 template <typename T, int D>
 int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
                 const void* v, const void* o, const void* dout, const float* lse, void* dq,
@@ -2821,7 +2865,11 @@ int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, con
     if constexpr (D == 64)
       if (c == kSP && sp_ok(d)) return dq_sp_launch<D>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
-      if (c == kP8 || c == kSP) return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+      if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dq))
+        return dq_asm_launch(d, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D == 64)
+      if (c == kP8 || c == kSP || c == kAsm)
+        return dq_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kP4N2) return dq_pipe_launch<T, D, 4, 2>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D <= 128)

@@ -1,0 +1,31 @@
+// vd_asm.h -- argument blocks and launchers of the hand-scheduled kernels
+// (asm/gen_attn_asm.py; asm_kernels.cpp).  Internal to libvdiff.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vd {
+
+// vd_attn_bwd_dq_d64 kernarg block (gen_attn_asm.py KARG layout, 128 bytes).  Byte
+// quantities are offsets from the sequence base; *_bytes ranges bound the buffer range
+// checks that zero-fill rows past the sequence end.
+struct AsmDqArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  const void* dout;
+  const float* nlse2;
+  const float* ndelta;
+  void* dq;
+  uint32_t n, ts_bytes, ots_bytes, groups;
+  uint64_t bs_bytes, gs_bytes, obs_bytes, ogs_bytes;
+  float scale, qscale;
+  uint32_t kv_bytes, o_bytes, tile_bytes, niter;
+};
+static_assert(sizeof(AsmDqArgs) == 128, "kernarg block layout");
+
+// grid (ceil(n / 256), groups, nseq / groups), 256 threads, 64 KiB static LDS
+int asm_bwd_dq_d64(const AsmDqArgs& a, unsigned gx, unsigned gy, unsigned gz,
+                   hipStream_t stream);
+
+}  // namespace vd

@@ -859,7 +859,7 @@ def cross_attention(q, kv, heads=1, frames=1, per_frame=True):
 
 
 ATTN_CONFIGS = {"auto": -1, "base": 0, "nb2": 1, "w8": 2, "p8": 3, "p4": 4, "d8": 5, "d8n": 6, "d4": 7,
-                "pair": 8, "p4n2": 9, "role": 10, "sp": 11}
+                "pair": 8, "p4n2": 9, "role": 10, "sp": 11, "asm": 12}
 
 
 class attention_config:
