@@ -131,6 +131,10 @@ class Stream:
         self.pending = []     # outstanding LDS read ids, issue order
         self.nops = 0
         self.waits = 0
+        self.forced = 0   # waits forced by the 15-read limit
+        self.young = 0    # ... of which waited on a read issued < 4 MFMAs earlier (a stall)
+        self.nmfma = 0
+        self.issued_at = {}
 
     def comment(self, text):
         self.lines.append(f"\t; {text}")
@@ -169,6 +173,17 @@ class Stream:
 
     def emit(self, text, lds_id=None, wait_lds=()):
         ins = Ins(text, lds_id, wait_lds)
+        if ins.lds_id is not None and len(self.pending) >= 15:
+            # lgkmcnt is a 4-bit counter: keep at most 15 LDS reads outstanding
+            k = 14
+            young = self.nmfma - self.issued_at.get(self.pending[0], -99) < 4
+            self.young += young
+            self.lines.append(f"\ts_waitcnt lgkmcnt({k})  ; forced: 15 reads in flight"
+                              + (" (young)" if young else ""))
+            self.pending = self.pending[len(self.pending) - k:]
+            self.pos += 1
+            self.waits += 1
+            self.forced += 1
         if ins.wait_lds:
             idx = [self.pending.index(i) for i in ins.wait_lds if i in self.pending]
             if idx:
@@ -187,6 +202,9 @@ class Stream:
         self.lines.append("\t" + ins.text)
         if ins.lds_id is not None:
             self.pending.append(ins.lds_id)
+            self.issued_at[ins.lds_id] = self.nmfma
+        if ins.kind == "mfma":
+            self.nmfma += 1
         if ins.kind in ("mfma", "valu", "trans"):
             self.hist.append((self.pos, ins))
             if len(self.hist) > 64:
@@ -203,13 +221,11 @@ class Stream:
 
 def kernel_text(name, body, *, vgprs, agprs, sgprs, lds_bytes, kernarg_bytes, wg_size,
                 wg_ids=(1, 1, 1)):
-    """A complete .s with one kernel (descriptor + HSA metadata, code object v5)."""
+    """(code + descriptor text, metadata entry) of one kernel (code object v5)."""
     accum = (vgprs + 3) // 4 * 4
     total = accum + agprs
     assert total <= 512, total
-    return f""".amdgcn_target "amdgcn-amd-amdhsa--gfx950"
-.amdhsa_code_object_version 5
-.text
+    code = f""".text
 .globl {name}
 .p2align 8
 .type {name},@function
@@ -240,12 +256,8 @@ def kernel_text(name, body, *, vgprs, agprs, sgprs, lds_bytes, kernarg_bytes, wg
   .amdhsa_ieee_mode 1
   .amdhsa_dx10_clamp 1
 .end_amdhsa_kernel
-
-.amdgpu_metadata
----
-amdhsa.version: [ 1, 2 ]
-amdhsa.kernels:
-  - .name: {name}
+"""
+    meta = f"""  - .name: {name}
     .symbol: {name}.kd
     .kernarg_segment_size: {kernarg_bytes}
     .group_segment_fixed_size: {lds_bytes}
@@ -258,6 +270,16 @@ amdhsa.kernels:
     .max_flat_workgroup_size: {wg_size}
     .args:
       - {{ .offset: 0, .size: {kernarg_bytes}, .value_kind: by_value }}
-...
-.end_amdgpu_metadata
 """
+    return code, meta
+
+
+def code_object_text(kernels, data=""):
+    """One .s holding several kernels: kernels = [(code, meta)], data = extra .rodata."""
+    out = '.amdgcn_target "amdgcn-amd-amdhsa--gfx950"\n.amdhsa_code_object_version 5\n'
+    out += "".join(c for c, _ in kernels)
+    out += data
+    out += "\n.amdgpu_metadata\n---\namdhsa.version: [ 1, 2 ]\namdhsa.kernels:\n"
+    out += "".join(m for _, m in kernels)
+    out += "...\n.end_amdgpu_metadata\n"
+    return out

@@ -2534,7 +2534,7 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
       !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
-      !(env == kAsm && (D != 64 || kind != 1)) &&    // hand-scheduled: D = 64 dQ
+      !(env == kAsm && (D != 64 || kind == 0)) &&    // hand-scheduled: D = 64 backward
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kind == 0 ? kD8N : kP8;
@@ -2842,6 +2842,33 @@ int dq_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const voi
   return rc ? rc : vd::check_launch("attn_bwd_dq");
 }
 
+int dkdv_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                    const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
+                    hipStream_t st) {
+  const int64_t n = d->seq_len;
+  vd::AsmDkdvArgs a{};
+  a.q = q; a.k = k; a.v = v; a.dout = dout; a.nlse2 = nlse2; a.ndelta = ndelta;
+  a.dk = dk; a.dv = dv;
+  a.n = (uint32_t)n;
+  a.ts_bytes = (uint32_t)(d->token_stride * 2);
+  a.ots_bytes = (uint32_t)(d->o_token_stride * 2);
+  a.groups = (uint32_t)d->groups;
+  a.bs_bytes = (uint64_t)d->batch_stride * 2;
+  a.gs_bytes = (uint64_t)d->group_stride * 2;
+  a.obs_bytes = (uint64_t)d->o_batch_stride * 2;
+  a.ogs_bytes = (uint64_t)d->o_group_stride * 2;
+  a.scale = d->scale;
+  a.kscale = d->scale * kLog2e;
+  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 64) * 2);
+  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 64) * 2);
+  a.tile_bytes = (uint32_t)(kTile * d->token_stride * 2);
+  a.otile_bytes = (uint32_t)(kTile * d->o_token_stride * 2);
+  a.niter = (uint32_t)vd_cdiv(vd_cdiv(n, kTile), 4);
+  const int rc = vd::asm_bwd_dkdv_d64(a, (unsigned)vd_cdiv(n, 256), (unsigned)d->groups,
+                                      (unsigned)(d->nseq / d->groups), st);
+  return rc ? rc : vd::check_launch("attn_bwd_dkdv");
+}
+
 template <typename T, int D>
 int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
                 const void* v, const void* o, const void* dout, const float* lse, void* dq,
@@ -2997,7 +3024,10 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
       if (c == kSP && sp_ok(d))
         return dkdv_sp_launch<D>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
-      if (c == kP8 || c == kSP)
+      if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dk) && asm_dq_ok(d, q, k, v, dout, dv))
+        return dkdv_asm_launch(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 64)
+      if (c == kP8 || c == kSP || c == kAsm)
         return dkdv_pipe_launch<T, D, 8>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kP4N2)

@@ -28,4 +28,25 @@ static_assert(sizeof(AsmDqArgs) == 128, "kernarg block layout");
 int asm_bwd_dq_d64(const AsmDqArgs& a, unsigned gx, unsigned gy, unsigned gz,
                    hipStream_t stream);
 
+// vd_attn_bwd_dkdv_d64 kernarg block (gen_attn_asm.py dK/dV layout, 144 bytes)
+struct AsmDkdvArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  const void* dout;
+  const float* nlse2;
+  const float* ndelta;
+  void* dk;
+  void* dv;
+  uint32_t n, ts_bytes, ots_bytes, groups;
+  uint64_t bs_bytes, gs_bytes, obs_bytes, ogs_bytes;
+  float scale, kscale;
+  uint32_t kv_bytes, o_bytes, tile_bytes, otile_bytes, niter, pad;
+};
+static_assert(sizeof(AsmDkdvArgs) == 144, "kernarg block layout");
+
+// grid (ceil(n / 256), groups, nseq / groups), 256 threads, 67 KiB static LDS
+int asm_bwd_dkdv_d64(const AsmDkdvArgs& a, unsigned gx, unsigned gy, unsigned gz,
+                     hipStream_t stream);
+
 }  // namespace vd

@@ -1,8 +1,8 @@
-"""The hand-scheduled head_dim-64 dQ kernel (vd_attn_bwd_dq_d64, csrc/asm/gen_attn_asm.py,
-attention config "asm") against the compiler-scheduled pipelined kernel (config "p8") on the
+"""The hand-scheduled head_dim-64 backward kernels (vd_attn_bwd_dq_d64 and
+vd_attn_bwd_dkdv_d64, csrc/asm/gen_attn_asm.py, attention config "asm") against the compiler-scheduled pipelined kernel (the default, config "auto") on the
 same bf16 inputs, and against a materialised fp32 reference of QKVAttentionLegacy's backward
 (unet.py:349-366).  The asm kernel runs the same products in the same accumulation order,
-so the two kernels' dQ agree bit for bit; dK / dV come from the same kernel in both runs.
+so dQ, dK and dV agree with the pipelined kernels' to fp32 rounding (bound 1e-6 rel-L2).
 Shapes: joint attention with whole and ragged last tiles, a batch of two sequences, and
 spatial grouping (4 frames x 1024 tokens: groups on grid.y) -- the kernel takes N >= 1024."""
 import math
@@ -35,29 +35,29 @@ def _inputs(B, N, seed, spatial=None):
 
 @pytest.mark.parametrize("B,N,seed", [(1, 1024, 0), (1, 4096, 1), (1, 5000, 2), (2, 3000, 3),
                                       (1, 65536 + 17, 4)])
-def test_asm_dq_equals_pipelined_kernel(B, N, seed):
+def test_asm_bwd_equals_pipelined_kernels(B, N, seed):
     qkv, g = _inputs(B, N, seed)
-    y0, g0 = _grads(qkv, g, "p8")
+    y0, g0 = _grads(qkv, g, "auto")
     y1, g1 = _grads(qkv, g, "asm")
-    assert torch.equal(y0, y1)
+    assert torch.equal(y0, y1)                     # the forward is not affected
     assert torch.isfinite(g1.float()).all()
-    assert torch.equal(g0[:, 64:], g1[:, 64:])     # dK / dV: same kernel
-    dq0, dq1 = g0[:, :64].float(), g1[:, :64].float()
-    assert dq1.abs().max() > 0
-    err = float((dq0 - dq1).norm() / dq0.norm())
-    assert err <= 1e-6, err
+    for name, sl in (("dq", slice(0, 64)), ("dk", slice(64, 128)), ("dv", slice(128, 192))):
+        a, b = g0[:, sl].float(), g1[:, sl].float()
+        assert b.abs().max() > 0, name
+        err = float((a - b).norm() / a.norm())
+        assert err <= 1e-6, (name, err)
 
 
-def test_asm_dq_spatial_groups():
+def test_asm_bwd_spatial_groups():
     qkv, g = _inputs(1, None, 5, spatial=(4, 32, 32))
     kw = dict(mode="spatial", spatial=(4, 32, 32))
-    _, g0 = _grads(qkv, g, "p8", **kw)
+    _, g0 = _grads(qkv, g, "auto", **kw)
     _, g1 = _grads(qkv, g, "asm", **kw)
-    err = float((g0[:, :64].float() - g1[:, :64].float()).norm() / g0[:, :64].float().norm())
+    err = float((g0.float() - g1.float()).norm() / g0.float().norm())
     assert err <= 1e-6, err
 
 
-def test_asm_dq_against_fp32_reference():
+def test_asm_bwd_against_fp32_reference():
     N, C = 4096, 64
     qkv, g = _inputs(1, N, 6)
     _, gr = _grads(qkv, g, "asm")
@@ -67,5 +67,6 @@ def test_asm_dq_against_fp32_reference():
     s = (q @ k.T) / math.sqrt(C)
     o = torch.softmax(s, -1) @ v
     o.backward(g.float()[0].T)
-    e = float((gr[0, :C].float().T - q.grad).norm() / q.grad.norm())
-    assert e < 2e-2, e
+    for got, ref in ((gr[0, :C], q.grad), (gr[0, C:2 * C], k.grad), (gr[0, 2 * C:], v.grad)):
+        e = float((got.float().T - ref).norm() / ref.norm())
+        assert e < 2e-2, e
