@@ -131,8 +131,9 @@ def prologue_dq(st: Stream, V, A):
     r(f"s_load_dwordx16 s[16:31], {S_KARG}, 0x0")
     r(f"s_load_dwordx16 s[32:47], {S_KARG}, 0x40")
     e(f"v_and_b32 {V.r('lane')}, 63, {V.r('tid')}")
-    e(f"v_lshrrev_b32 {V.r('tmp')}, 6, {V.r('tid')}")
-    r(f"v_readfirstlane_b32 {S_WAVE}, {V.r('tmp')}")
+    r(f"v_readfirstlane_b32 {S_WAVE}, {V.r('tid')}")  # first lane's id = 64 * wave
+    r("s_nop 1")
+    r(f"s_lshr_b32 {S_WAVE}, {S_WAVE}, 6")
     r("s_getpc_b64 s[88:89]")
     r("s_add_u32 s88, s88, vd_attn_dq_lanes@rel32@lo+4")
     r("s_addc_u32 s89, s89, vd_attn_dq_lanes@rel32@hi+12")
@@ -555,8 +556,9 @@ def prologue_dkdv(st: Stream, V, A):
     r(f"s_load_dwordx16 s[32:47], {S_KARG}, 0x40")
     r(f"s_load_dwordx4 s[48:51], {S_KARG}, 0x80")
     e(f"v_and_b32 {V.r('lane')}, 63, {V.r('tid')}")
-    e(f"v_lshrrev_b32 {V.r('tmp')}, 6, {V.r('tid')}")
-    r(f"v_readfirstlane_b32 {S2_WAVE}, {V.r('tmp')}")
+    r(f"v_readfirstlane_b32 {S2_WAVE}, {V.r('tid')}")  # first lane's id = 64 * wave
+    r("s_nop 1")
+    r(f"s_lshr_b32 {S2_WAVE}, {S2_WAVE}, 6")
     r("s_getpc_b64 s[96:97]")
     r("s_add_u32 s96, s96, vd_attn_dkdv_lanes@rel32@lo+4")
     r("s_addc_u32 s97, s97, vd_attn_dkdv_lanes@rel32@hi+12")

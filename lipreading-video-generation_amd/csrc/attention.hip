@@ -1448,101 +1448,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(
 #ifndef VD_BWD_STAGGER
 #define VD_BWD_STAGGER 1
 #endif
-#ifdef VD_ATTN_SCHED
-constexpr bool kSchedOn = true;
-#else
-constexpr bool kSchedOn = false;
-#endif
-// per block: LDS reads / MFMAs of S, LDS reads of G, G MFMAs with the softmax VALU spread
-template <int D> using DkdvSched = BlockSched<16, 8, 4 * D / 16, D / 8, 48 / (D / 8)>;
-template <int D> using DqSched = BlockSched<8, 8, D / 8, D / 16, 40 / (D / 16)>;
 
 
 // Same math as the kernels above (one 32-row block per wave, NB = 1), on tile_pipe.
 
-template <typename T, int D, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
-    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
-    float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
-  const int seq = blockIdx.y;
-  const int q0 = blockIdx.x * (32 * NW) + wave * 32;
-  const int64_t base = qa(seq);
-  const bool late = NW == 8 && wave >= 4;
-
-  RowFrag<T, D> qf;
-  qf.load(q + base, ts, q0 + (lane & 31), n, lane);
-  qf.scale(scale * kLog2e);
-  f32x16 oacc[D / 32];
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
-  float m = -INFINITY, l = 0.f;
-  f32x16 negm, s;
-  XOp<T> p{};  // zero: the G step before the first softmax adds nothing
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    negm[r] = INFINITY;
-    s[r] = -INFINITY;  // a late wave's V(-1) then yields p = 0, psum = 0
-  }
-
-  auto mask = [&](int key0) {
-    if (key0 + 32 > n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (key0 + acc_row(r, hh) >= n) s[r] = -INFINITY;
-  };
-  tile_pipe<T, D, false, NW>(
-      smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
-      [&](const BlockRef<T>& bs) {
-        s = negm;
-        mma_rows<T, D>(s, bs.a, bs.row0, qf, lane);
-      },
-      [&](const BlockRef<T>& bg) {
-#pragma unroll
-        for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], bg.b, bg.row0, 32 * i, p, lane);
-      },
-      [&](const BlockRef<T>& bv) {
-        mask(32 * bv.idx);
-        float psum = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          s[r] = fast_exp2(s[r]);
-          psum += s[r];
-        }
-        if (!__all(psum < kLagSum)) {  // rare: redo the block against its true max
-          s = f32x16{};
-          mma_rows<T, D>(s, bv.a, bv.row0, qf, lane);
-          mask(32 * bv.idx);
-          float tmax = s[0];
-#pragma unroll
-          for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, s[r]);
-          tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-          const float mnew = fmaxf(m, tmax);
-          const float alpha = fast_exp2(m - mnew);
-          m = mnew;
-          l *= alpha;
-#pragma unroll
-          for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) negm[r] = -mnew;
-          psum = 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            s[r] = fast_exp2(s[r] - mnew);
-            psum += s[r];
-          }
-        }
-        l += psum;
-        p = XOp<T>(s);
-      });
-  const int myq = q0 + (lane & 31);
-  const float lt = l + __shfl_xor(l, 32, 64);
-  store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, oacc, 1.f / lt, lane);
-  if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m + log2f(lt)) / kLog2e;
-}
 
 // Forward with the lagged-max check deferred to the tile boundary, so the loop body is one
 // basic block.  PV runs one tile (two 32-key blocks) behind the softmax: the check of tile
@@ -1553,40 +1462,11 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_fwd_pipe_kernel(
 // staggered waves 4-7: V(2t-1) [check(t-1)] S(2t) G(2t-2) V(2t) S(2t+1) G(2t-1).
 // Same ring as tile_pipe (4 stages, prefetch distance 2): tile t-1 stays resident while
 // t+1 and t+2 land.  bf16, D = 64 (the issue-bound shape).
-#ifndef VD_DEFER_PRE
-#define VD_DEFER_PRE 0
-#endif
-// VD_DEFER_MSUM=1: row sums on the matrix pipe (below).  Correct, but measured 22.1 vs
-// 18.0 ms at N = 262144: the 16x16x32 sum MFMAs sit on the exp -> cvt -> MFMA chain and
-// serialise on their accumulator.  Kept as an A/B build flag; off.
-#ifndef VD_DEFER_MSUM
-#define VD_DEFER_MSUM 0
-#endif
-#ifndef VD_DEFER_TREE
-#define VD_DEFER_TREE 1
-#endif
-// VD_DEFER_B2 (A/B, D = 64 with 8 waves): an 8-stage ring with one barrier per TWO tiles
-// (prefetch distance 4, two tiles issued per barrier), so the SIMD partners re-align at
-// half as many barriers.
-#ifndef VD_DEFER_B2
-#define VD_DEFER_B2 0
-#endif
-template <int D, int NW> constexpr bool defer_b2() { return VD_DEFER_B2 && D == 64 && NW == 8; }
-// VD_DEFER_IGLP (A/B): the softmax of block 2t (V(sa)) spread over the MFMAs of S(2t+1) and
-// G(2t-1) -- NV VALU per MFMA (sched_group_barrier), the region fenced by sched_barriers --
-// instead of the compiler's clusters of 6-7 v_exp between two MFMAs.
-#ifndef VD_DEFER_IGLP
-#define VD_DEFER_IGLP 0
-#endif
-template <int NM, int NV>
-__device__ __forceinline__ void defer_interleave() {
-#pragma unroll
-  for (int i = 0; i < NM; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-  }
-}
-template <int D, int NW> constexpr int defer_nst() { return defer_b2<D, NW>() ? 8 : 4; }
+// Measured and retired (profiles/r01_ab_*, r02_ab_defer_*): every LDS fragment of the body
+// loaded up front (18.0 vs 17.4 ms), row sums on the matrix pipe (22.1 vs 18.0 ms: the sum
+// MFMAs serialise on the exp -> cvt -> MFMA chain), one barrier per two tiles (17.4 vs 16.7
+// ms), the softmax spread by sched_group_barrier (15.4-15.6 vs 15.3 ms).
+template <int D, int NW> constexpr int defer_nst() { return 4; }
 
 template <typename T, int D, int NW, bool STAGGER>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
@@ -1594,8 +1474,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     float* __restrict__ lse, int n, SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
   static_assert(kDMA<T> && (D == 64 || D == 128), "deferred-check forward: bf16, D = 64 / 128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr bool B2 = defer_b2<D, NW>();
-  constexpr int TE = kTile * D, NST = defer_nst<D, NW>(), PD = B2 ? 4 : 2;
+  constexpr int TE = kTile * D, NST = defer_nst<D, NW>(), PD = 2;
   constexpr int STAGE_BYTES = pipe_stage_bytes<D, false, kTile>();
   constexpr int PER_TILE = 2 * dma_ipw<D, NW, kTile>();
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
@@ -1612,22 +1491,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
   float m = -INFINITY;
-#if VD_DEFER_MSUM
-  // Row sums on the matrix pipe instead of 32 v_add per tile: a 16x16x32 MFMA with a 0/1
-  // selector as A and a block's P^T register as B.  As a 16x16x32 B operand, lane l of P^T
-  // (query l % 32) lands in column l % 16, k-group l / 16; selector row 0 takes k-groups
-  // 0 and 2 (queries 0-15), row 1 k-groups 1 and 3 (queries 16-31).  So lanes 0-15 hold
-  // the sums of query n in [0] and of query n + 16 in [1] (the bf16 P that PV uses).
-  const short one = (lane == 0 || lane == 32 || lane == 17 || lane == 49) ? (short)0x3F80 : 0;
-  const bf16x8 sel = bf16x8{one, one, one, one, one, one, one, one};
-  f32x4 lsum = f32x4{}, tsum = f32x4{};  // running / pending-tile row sums
-  auto V_sum = [&](const XOp<T>& p) __attribute__((always_inline)) {
-    tsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, p.b[0], tsum, 0, 0, 0);
-    tsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, p.b[1], tsum, 0, 0, 0);
-  };
-#else
   float l = 0.f, psa = 0.f, psb = 0.f;
-#endif
   f32x16 negm, sa, sb;
   XOp<T> pa{}, pb{};  // zero: G(-2), G(-1) add nothing
 #pragma unroll
@@ -1667,21 +1531,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     for (int i = 0; i < D / 32; ++i) mma_tr<T, D>(oacc[i], vb, 32 * (bi & 1), 32 * i, p, lane);
   };
   // MK: the block may hold keys >= n (only the last tile's blocks can)
-#if VD_DEFER_MSUM
-  auto V = [&](f32x16& s, XOp<T>& p, float&, int bi, auto mk) __attribute__((always_inline)) {
-    if constexpr (decltype(mk)::value) mask(s, bi);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = fast_exp2(s[r]);
-    p = XOp<T>(s);
-    V_sum(p);
-  };
-  float psa = 0.f, psb = 0.f;  // unused (sums on the matrix pipe)
-#else
   auto V = [&](f32x16& s, XOp<T>& p, float& ps, int bi, auto mk) __attribute__((always_inline)) {
     if constexpr (decltype(mk)::value) mask(s, bi);
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = fast_exp2(s[r]);
-#if VD_DEFER_TREE
     // pairwise: a 4-deep dependency chain instead of 16 (A/B build flag)
     float t8[8];
 #pragma unroll
@@ -1689,21 +1542,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) t8[r] = t8[2 * r] + t8[2 * r + 1];
     ps = (t8[0] + t8[1]) + (t8[2] + t8[3]);
-#else
-    ps = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ps += s[r];
-#endif
     p = XOp<T>(s);
   };
-#endif
   // blocks 2tp, 2tp+1 hold p against the current m; their PV has not run yet
   auto check = [&](int tp) __attribute__((always_inline)) {
-#if VD_DEFER_MSUM
-    const bool ok = lane >= 16 || (tsum[0] < kLagSum && tsum[1] < kLagSum);
-#else
     const bool ok = psa < kLagSum && psb < kLagSum;
-#endif
     if (!__all(ok)) {  // rare: true max of the tile
       // sa / sb are dead here (their blocks' softmax ran): reuse them, no extra registers
       f32x16& s0 = sa;
@@ -1721,16 +1564,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
       const float mnew = fmaxf(m, tmax);
       const float alpha = fast_exp2(m - mnew);  // m = -inf: 0 (O and l are 0 then)
       m = mnew;
-#if VD_DEFER_MSUM
-      // lanes 0-15 hold query n in [0] and query n + 16 in [1]: the latter's alpha is on
-      // lane n + 16
-      const float alpha1 = __shfl(alpha, (lane & 15) + 16, 64);
-      lsum[0] *= alpha;
-      lsum[1] *= alpha1;
-      tsum = f32x4{};
-#else
       l *= alpha;
-#endif
 #pragma unroll
       for (int i = 0; i < D / 32; ++i)
 #pragma unroll
@@ -1744,12 +1578,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
       V(s0, pa, psa, 2 * tp, std::false_type{});  // masked above
       V(s1, pb, psb, 2 * tp + 1, std::false_type{});
     }
-#if VD_DEFER_MSUM
-    lsum += tsum;
-    tsum = f32x4{};
-#else
     l += psa + psb;
-#endif
   };
 
   {  // zero the stage that stands in for tile -1
@@ -1769,68 +1598,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
     constexpr int SG = decltype(sg_c)::value;
     const char* cur = SG >= 0 ? smem + SG * STAGE_BYTES : nullptr;
     const char* prv = SG >= 0 ? smem + ((SG + NST - 1) % NST) * STAGE_BYTES : nullptr;
-    if constexpr (B2) {  // even tiles: t, t+1 landed; t-4, t-3 no longer read
-      if (SG >= 0 ? (SG & 1) == 0 : (t & 1) == 0) {
-        vm_wait_barrier<2 * PER_TILE>();
-        issue(t + PD);
-        issue(t + PD + 1);
-      }
-    } else {
-      vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
-      issue(t + PD);
-    }
+    vm_wait_barrier<(PD - 1) * PER_TILE>();  // tile t landed; tile t-2 no longer read
+    issue(t + PD);
     const int b0 = 2 * t;
     if constexpr (LATE) V(sb, pb, psb, b0 - 1, std::false_type{});
     check(t - 1);
-#if VD_DEFER_PRE
-    // every LDS fragment of the body up front (K rows of tile t, V^T of tile t-1; 64 VGPRs),
-    // so no MFMA waits on a just-issued read
-    bf16x8 kf[2][D / 16], vf[2][D / 32][2];
-    {
-      const T* Kt = kblk(b0);
-      const T* Vp = vblk(b0 - 2);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int ss = 0; ss < D / 16; ++ss)
-          kf[h][ss] = *reinterpret_cast<const bf16x8*>(
-              Kt + toff<T, D>(32 * h + (lane & 31), 16 * ss + 8 * hh));
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < D / 32; ++i) load_tr<D>(vf[h][i], Vp, 32 * h, 32 * i, lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    auto Sp = [&](f32x16& s, int h) __attribute__((always_inline)) {
-      s = negm;
-#pragma unroll
-      for (int ss = 0; ss < D / 16; ++ss)
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[h][ss], qf.f[ss], s, 0, 0, 0);
-    };
-    auto Gp = [&](const XOp<T>& p, int h) __attribute__((always_inline)) {
-#pragma unroll
-      for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          oacc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[h][i][s2], p.b[s2], oacc[i], 0, 0, 0);
-    };
-    Sp(sa, 0);
-    Gp(pa, 0);
-    V(sa, pa, psa, b0, mk);
-    Sp(sb, 1);
-    Gp(pb, 1);
-#else
     S(sa, b0, cur);
     G(pa, b0 - 2, prv);
-    if constexpr (VD_DEFER_IGLP && D == 64 && !decltype(mk)::value) __builtin_amdgcn_sched_barrier(0);
     V(sa, pa, psa, b0, mk);
     S(sb, b0 + 1, cur);
     G(pb, b0 - 1, prv);
-    if constexpr (VD_DEFER_IGLP && D == 64 && !decltype(mk)::value) {
-      defer_interleave<2 * (D / 16), VD_DEFER_IGLP>();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
     if constexpr (!LATE) V(sb, pb, psb, b0 + 1, mk);
   };
   auto run = [&](auto late_c) __attribute__((always_inline)) {
@@ -1844,12 +1621,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
       tile(t + 1, late_c, std::false_type{}, std::integral_constant<int, 1>{});
       tile(t + 2, late_c, std::false_type{}, std::integral_constant<int, 2>{});
       tile(t + 3, late_c, std::false_type{}, std::integral_constant<int, 3>{});
-      if constexpr (NST == 8) {
-        tile(t + 4, late_c, std::false_type{}, std::integral_constant<int, 4>{});
-        tile(t + 5, late_c, std::false_type{}, std::integral_constant<int, 5>{});
-        tile(t + 6, late_c, std::false_type{}, std::integral_constant<int, 6>{});
-        tile(t + 7, late_c, std::false_type{}, std::integral_constant<int, 7>{});
-      }
     }
 #endif
     for (; t < ntiles - 1; ++t) tile(t, late_c, std::false_type{}, Dyn{});
@@ -1867,12 +1638,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_defer_kernel(
   vm_drain();
 
   const int myq = q0 + (lane & 31);
-#if VD_DEFER_MSUM
-  const float l0 = __shfl(lsum[0], lane & 15, 64), l1 = __shfl(lsum[1], lane & 15, 64);
-  const float lt = (lane & 16) ? l1 : l0;
-#else
   const float lt = l + __shfl_xor(l, 32, 64);
-#endif
   store_transposed<T, D / 32>(o + oa(seq), ots, myq, n, 0, oacc, 1.f / lt, lane);
   if (hh == 0 && myq < n) lse[(int64_t)seq * n + myq] = (m + log2f(lt)) / kLog2e;
 }
@@ -1923,7 +1689,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
   // at N = 262144 (dK/dV measured no gain, so it stays off there)
   if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
-  tile_pipe<T, D, false, NW, typename std::conditional<kSchedOn && NB == 1, DqSched<D>, NoSched>::type,
+  tile_pipe<T, D, false, NW, NoSched,
             pipe_tr<D, NW>()>(
       smem, k + base, v + base, ts, ts, nullptr, nullptr, n, tid, late,
       [&](const BlockRef<T>& bs) {
@@ -1990,7 +1756,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);  // A/B: as the dQ kernel
 #endif
 
-  tile_pipe<T, D, true, NW, typename std::conditional<kSchedOn && NB == 1, DkdvSched<D>, NoSched>::type,
+  tile_pipe<T, D, true, NW, NoSched,
             pipe_tr<D, NW>()>(
       smem, q + base, dout + obase, ts, ots, nlse2 + (int64_t)seq * n, ndelta + (int64_t)seq * n,
       n, tid, late,
@@ -2046,424 +1812,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_pipe_kernel(
   }
 }
 
-// ================================================================== fragment-pipelined backward
-// (round 2, cfg "sp", the head_dim-64 default).  The compiler schedules every LDS fragment
-// read of the kernels above right before its MFMA behind an lgkmcnt(0) (tools/kseq.py: the
-// 'R W M' pattern), so each MFMA of a wave waits a full LDS latency; with one wave per SIMD
-// (p4n2) the matrix pipe idles about as long as it works.  Here the reads of the NEXT MFMA
-// group are issued before the current group, and sched_barriers pin MFMAs and LDS reads in
-// that order while VALU / SALU / transcendental work may move across them (mask 0x406), so
-// the softmax still fills the MFMA gaps.  One wave per SIMD: 4 waves x 2 blocks of 32 rows
-// (64 keys per wave for dK/dV, 64 queries for dQ) with the whole 512-register file.
-// MFMA-group order per 64-row tile t (blocks b0 = 2t, b1 = 2t + 1):
-//   [wait + barrier] R:S(b0) M:G(b0-2) R:G(b0-1) M:S(b0) R:S(b1) M:G(b0-1) R:G(b0) M:S(b1)
-// S(b): the block's score products; G(b): its gradient products, two groups later, so the
-// softmax of block b (V(b)) has the G(b-1) and S(b+1) groups (32 MFMAs) to hide in; s / dp
-// and P / dS are kept per block parity.  R:S(b) reads tile t only, R:G(b0-1) tile t-1 (still
-// resident: the ring keeps t-1, t while t+1, t+2 land).
-#ifndef VD_SP_MASK
-#define VD_SP_MASK 0
-#endif
-#define VD_SP_FENCE() __builtin_amdgcn_sched_barrier(VD_SP_MASK)
-#ifndef VD_SP_PRIO  // A/B: static priority for the second wave half (8 waves)
-#define VD_SP_PRIO 0
-#endif
-#ifndef VD_SP_NV
-#define VD_SP_NV 3
-#endif
-#ifndef VD_SP_NVG  // dK/dV: the whole softmax of a block in one G group
-#define VD_SP_NVG 6
-#endif
-// An MFMA group region: NM x {1 MFMA, NV VALU} (the softmax half placed in the region)
-#ifndef VD_SP_IGLP
-#define VD_SP_IGLP 1
-#endif
-template <int NM, int NV>
-__device__ __forceinline__ void sp_interleave() {
-  if constexpr (!VD_SP_IGLP) return;
-#pragma unroll
-  for (int i = 0; i < NM; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-  }
-}
-
-// Row fragments of a 32-row block over D (the A operand of S = rows . frag^T)
-template <int D>
-__device__ __forceinline__ void sp_rows(bf16x8 (&f)[D / 16], const bf16_t* tile, int row0,
-                                        int lane) {
-  const int r = row0 + (lane & 31), hh = lane >> 5;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s)
-    f[s] = *reinterpret_cast<const bf16x8*>(tile + toff<bf16_t, D>(r, 16 * s + 8 * hh));
-}
-// accumulator-layout row constants of a 32-row block (register 4g+e = row 8g + 4hh + e)
-__device__ __forceinline__ f32x16 sp_rowc(const float* rc, int row0, int lane) {
-  const int hh = lane >> 5;
-  f32x16 x;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const float4 v = *reinterpret_cast<const float4*>(rc + row0 + 8 * g + 4 * hh);
-    x[4 * g + 0] = v.x; x[4 * g + 1] = v.y; x[4 * g + 2] = v.z; x[4 * g + 3] = v.w;
-  }
-  return x;
-}
-
-template <int D, int NW, int NB>
-__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv_sp_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    const bf16_t* __restrict__ dout, const float* __restrict__ nlse2,
-    const float* __restrict__ ndelta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int n,
-    SeqAddr qa, int64_t ts, SeqAddr oa, int64_t ots, float scale) {
-  static_assert(D == 64 && (NB == 1 || NB == 2), "fragment pipeline: D = 64, 1-2 blocks");
-  using T = bf16_t;
-  constexpr int NST = 4, TE = kTile * D;
-  constexpr int NMG = 2 * NB * (D / 32) * 2;  // MFMAs per G group
-  constexpr int STAGE_BYTES = pipe_stage_bytes<D, true, kTile>();
-  constexpr int PER_TILE = 2 * dma_ipw<D, NW, kTile>() + 1;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int seq = blockIdx.y;
-  const int k0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
-  const int64_t base = qa(seq), obase = oa(seq);
-  const int ntiles = (n + kTile - 1) / kTile;
-
-  RowFrag<T, D> kf[NB], vf[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    kf[j].load(k + base, ts, k0 + 32 * j + (lane & 31), n, lane);
-    kf[j].scale(scale * kLog2e);
-    vf[j].load(v + base, ts, k0 + 32 * j + (lane & 31), n, lane);
-  }
-  // One set of S / dP accumulators: the row constants (-lse', -delta) of block b are read
-  // straight into them (once per key block: a shared copy would cost 32 registers or 32
-  // moves) at the head of R:G(b-1), after V(b-1) consumed them.  One set of P / dS
-  // operands: G(b) reads them one group after V(b) wrote them, in the group where V(b+1)
-  // overwrites them.
-  f32x16 adv[D / 32][NB], adk[D / 32][NB], s[NB], dp[NB];
-  XOp<T> pp[NB], ds[NB];  // zero: G(-2), G(-1) add nothing
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) adv[i][j] = adk[i][j] = f32x16{};
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    pp[j] = ds[j] = XOp<T>(f32x16{});
-    dp[j] = f32x16{};  // V(-1) in the first step: p = 0, dS = 0
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[j][r] = -INFINITY;
-  }
-  bf16x8 fa[D / 16], fb[D / 16];      // R:S -- Q rows, dO rows of the block
-  bf16x8 gv[D / 32][2], gk[D / 32][2];  // R:G -- dO^T, Q^T fragments of the block
-
-  const auto ra = make_rsrc(q + base, seq_bytes(n, ts, D, 2));
-  const auto rb = make_rsrc(dout + obase, seq_bytes(n, ots, D, 2));
-  const auto r0 = make_rsrc(nlse2 + (int64_t)seq * n, (uint32_t)n * 4u);
-  const auto r1 = make_rsrc(ndelta + (int64_t)seq * n, (uint32_t)n * 4u);
-  const uint32_t tsa = (uint32_t)(ts * 2), tsb = (uint32_t)(ots * 2);
-  auto issue = [&](int t) __attribute__((always_inline)) {
-    char* st = smem + (t & (NST - 1)) * STAGE_BYTES;
-    const int tok0 = t * kTile;
-    dma_tile<D, NW, kTile>(ra, st, tok0, n, tsa, wave, lane);
-    dma_tile<D, NW, kTile>(rb, st + TE * 2, tok0, n, tsb, wave, lane);
-    // waves 0 / 1 stage the two row constants, waves 2 / 3 a throw-away copy (one vmcnt)
-    char* rcs = st + 4 * TE + (wave < 2 ? wave * kTile * 4 : 2 * kTile * 4);
-    dma_rowc(wave == 1 ? r1 : r0, rcs, tok0, lane);
-  };
-  auto tA = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES); };
-  auto tB = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES + TE * 2); };
-  auto tR = [&](int sg) { return reinterpret_cast<const float*>(smem + sg * STAGE_BYTES + 4 * TE); };
-  auto readS = [&](int sg, int row0) __attribute__((always_inline)) {
-    sp_rows<D>(fa, tA(sg), row0, lane);
-    sp_rows<D>(fb, tB(sg), row0, lane);
-  };
-  auto readRC = [&](int sg, int row0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      s[j] = sp_rowc(tR(sg), row0, lane);
-      dp[j] = sp_rowc(tR(sg) + kTile, row0, lane);
-    }
-  };
-  auto readG = [&](int sg, int row0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i) {
-      load_tr<D>(gv[i], tB(sg), row0, 32 * i, lane);
-      load_tr<D>(gk[i], tA(sg), row0, 32 * i, lane);
-    }
-  };
-  auto mmaS = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int ss = 0; ss < D / 16; ++ss)
-#pragma unroll
-      for (int j = 0; j < NB; ++j)
-        s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ss], kf[j].f[ss], s[j], 0, 0, 0);
-#pragma unroll
-    for (int ss = 0; ss < D / 16; ++ss)
-#pragma unroll
-      for (int j = 0; j < NB; ++j)
-        dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ss], vf[j].f[ss], dp[j], 0, 0, 0);
-  };
-  auto mmaG = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          adv[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[i][s2], pp[j].b[s2], adv[i][j], 0, 0, 0);
-          adk[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gk[i][s2], ds[j].b[s2], adk[i][j], 0, 0, 0);
-        }
-  };
-  auto softmax = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s[j][r] = fast_exp2(s[j][r]);
-        dp[j][r] *= s[j][r];
-      }
-      pp[j] = XOp<T>(s[j]);
-      ds[j] = XOp<T>(dp[j]);
-    }
-  };
-
-  {  // stage NST-1 stands in for tile -1 (zero rows: G(-1) reads it)
-    uint4* z = reinterpret_cast<uint4*>(smem + (NST - 1) * STAGE_BYTES);
-    for (int i = tid; i < STAGE_BYTES / 16; i += 64 * NW) z[i] = make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  if (VD_SP_PRIO && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  vm_drain();
-  issue(0);
-  issue(1);
-  readG(NST - 1, 0);  // G(-2): zero fragments of the zeroed stage
-  // tile step with a compile-time ring stage SG (the loop is unrolled by NST; tiles past the
-  // end are zero rows with zero row constants and add nothing, so the count is rounded up)
-  auto step = [&](int t, auto sg_c) __attribute__((always_inline)) {
-    constexpr int SG = decltype(sg_c)::value, SP = (SG + NST - 1) % NST;
-    vm_wait_barrier<PER_TILE>();  // tile t landed; tile t-2 no longer read
-    issue(t + 2);
-    VD_SP_FENCE();
-    readS(SG, 0);                 // R:S(b0)
-    VD_SP_FENCE();
-    mmaG();                       // M:G(b0-2) + V(b0-1)
-    softmax();
-    sp_interleave<NMG, VD_SP_NVG>();
-    VD_SP_FENCE();
-    readRC(SG, 0);                // R:G(b0-1), headed by the row constants of b0
-    readG(SP, 32);
-    VD_SP_FENCE();
-    mmaS();                       // M:S(b0)
-    VD_SP_FENCE();
-    readS(SG, 32);                // R:S(b1)
-    VD_SP_FENCE();
-    mmaG();                       // M:G(b0-1) + V(b0)
-    softmax();
-    sp_interleave<NMG, VD_SP_NVG>();
-    VD_SP_FENCE();
-    readRC(SG, 32);               // R:G(b0), headed by the row constants of b1
-    readG(SG, 0);
-    VD_SP_FENCE();
-    mmaS();                       // M:S(b1)
-    VD_SP_FENCE();
-  };
-  const int nt = (ntiles + NST - 1) / NST * NST;
-  for (int t = 0; t < nt; t += NST) {
-    step(t, std::integral_constant<int, 0>{});
-    step(t + 1, std::integral_constant<int, 1>{});
-    step(t + 2, std::integral_constant<int, 2>{});
-    step(t + 3, std::integral_constant<int, 3>{});
-  }
-  mmaG();  // G(2nt-2) (fragments already read) + V(2nt-1), then G(2nt-1)
-  softmax();
-  readG((nt - 1) & (NST - 1), 32);
-  mmaG();
-  vm_drain();
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int mykey = k0 + 32 * j + (lane & 31);
-    f32x16 ok[D / 32], ov[D / 32];
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i) {
-      ok[i] = adk[i][j];
-      ov[i] = adv[i][j];
-    }
-    store_transposed<T, D / 32>(dk + base, ts, mykey, n, 0, ok, scale, lane);
-    store_transposed<T, D / 32>(dv + base, ts, mykey, n, 0, ov, 1.f, lane);
-  }
-}
-
-// dQ on the same fragment pipeline: 64 queries per wave (2 blocks); K / V tiles stream.
-// S(b): S^T = K Q^T and dP^T = V dO^T from K / V rows; G(b): dQ^T += K^T dS^T (K^T by
-// transposed reads of the K tile).
-template <int D, int NW, int NB>
-__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_sp_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    const bf16_t* __restrict__ dout, const float* __restrict__ nlse2,
-    const float* __restrict__ ndelta, bf16_t* __restrict__ dq, int n, SeqAddr qa, int64_t ts,
-    SeqAddr oa, int64_t ots, float scale) {
-  static_assert(D == 64 && (NB == 1 || NB == 2), "fragment pipeline: D = 64, 1-2 blocks");
-  using T = bf16_t;
-  constexpr int NST = 4, TE = kTile * D;
-  constexpr int NMS = 2 * NB * (D / 16), NMG = NB * (D / 32) * 2;  // MFMAs per S / G group
-  constexpr int STAGE_BYTES = pipe_stage_bytes<D, false, kTile>();
-  constexpr int PER_TILE = 2 * dma_ipw<D, NW, kTile>();
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int seq = blockIdx.y;
-  const int q0 = blockIdx.x * (32 * NB * NW) + wave * 32 * NB;
-  const int64_t base = qa(seq);
-  const int ntiles = (n + kTile - 1) / kTile;
-
-  RowFrag<T, D> qf[NB], of[NB];
-  f32x16 il[NB], id[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int myq = q0 + 32 * j + (lane & 31);
-    qf[j].load(q + base, ts, myq, n, lane);
-    qf[j].scale(scale * kLog2e);
-    of[j].load(dout + oa(seq), ots, myq, n, lane);
-    const float a = myq < n ? nlse2[(int64_t)seq * n + myq] : 0.f;
-    const float b = myq < n ? ndelta[(int64_t)seq * n + myq] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      il[j][r] = a;
-      id[j][r] = b;
-    }
-  }
-  f32x16 acc[D / 32][NB], s[2][NB], dp[2][NB];
-  XOp<T> ds[2][NB];
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) ds[p][j] = XOp<T>(f32x16{});
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {  // V(-1) in the first step: dS = 0
-    dp[1][j] = f32x16{};
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[1][j][r] = -INFINITY;
-  }
-  bf16x8 fa[D / 16], fb[D / 16];  // R:S -- K rows, V rows of the block
-  bf16x8 gk[D / 32][2];           // R:G -- K^T fragments of the block
-
-  const auto ra = make_rsrc(k + base, seq_bytes(n, ts, D, 2));
-  const auto rb = make_rsrc(v + base, seq_bytes(n, ts, D, 2));
-  const uint32_t tsb = (uint32_t)(ts * 2);
-  auto issue = [&](int t) __attribute__((always_inline)) {
-    char* st = smem + (t & (NST - 1)) * STAGE_BYTES;
-    dma_tile<D, NW, kTile>(ra, st, t * kTile, n, tsb, wave, lane);
-    dma_tile<D, NW, kTile>(rb, st + TE * 2, t * kTile, n, tsb, wave, lane);
-  };
-  auto tA = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES); };
-  auto tB = [&](int sg) { return reinterpret_cast<const T*>(smem + sg * STAGE_BYTES + TE * 2); };
-  auto readS = [&](int sg, int row0) __attribute__((always_inline)) {
-    sp_rows<D>(fa, tA(sg), row0, lane);
-    sp_rows<D>(fb, tB(sg), row0, lane);
-  };
-  auto readG = [&](int sg, int row0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i) load_tr<D>(gk[i], tA(sg), row0, 32 * i, lane);
-  };
-  auto mmaS = [&](int par) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      s[par][j] = il[j];
-      dp[par][j] = id[j];
-    }
-#pragma unroll
-    for (int ss = 0; ss < D / 16; ++ss)
-#pragma unroll
-      for (int j = 0; j < NB; ++j)
-        s[par][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ss], qf[j].f[ss], s[par][j], 0, 0, 0);
-#pragma unroll
-    for (int ss = 0; ss < D / 16; ++ss)
-#pragma unroll
-      for (int j = 0; j < NB; ++j)
-        dp[par][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ss], of[j].f[ss], dp[par][j], 0, 0, 0);
-  };
-  auto mmaG = [&](int par) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gk[i][s2], ds[par][j].b[s2], acc[i][j], 0, 0, 0);
-  };
-  // half h of V(b): block h (NB = 2), or registers 8h..8h+7 of the one block (NB = 1)
-  auto softmax = [&](int par, int h) __attribute__((always_inline)) {
-    const int j = NB == 2 ? h : 0, r0 = NB == 2 ? 0 : 8 * h, r1 = NB == 2 ? 16 : 8 * h + 8;
-#pragma unroll
-    for (int r = r0; r < r1; ++r) s[par][j][r] = fast_exp2(s[par][j][r]) * dp[par][j][r];
-    if (NB == 2 || h == 1) ds[par][j] = XOp<T>(s[par][j]);
-  };
-
-  {  // stage NST-1 stands in for tile -1
-    uint4* z = reinterpret_cast<uint4*>(smem + (NST - 1) * STAGE_BYTES);
-    for (int i = tid; i < STAGE_BYTES / 16; i += 64 * NW) z[i] = make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  if (VD_SP_PRIO && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  vm_drain();
-  issue(0);
-  issue(1);
-  readG(NST - 1, 0);
-  auto step = [&](int t, auto sg_c) __attribute__((always_inline)) {
-    constexpr int SG = decltype(sg_c)::value, SP = (SG + NST - 1) % NST;
-    vm_wait_barrier<PER_TILE>();  // tile t landed; tile t-2 no longer read
-    issue(t + 2);
-    VD_SP_FENCE();
-    readS(SG, 0);                 // R:S(b0)
-    VD_SP_FENCE();
-    mmaG(0);                      // M:G(b0-2) + the first half of V(b0-1)
-    softmax(1, 0);
-    sp_interleave<NMG, VD_SP_NV>();
-    VD_SP_FENCE();
-    readG(SP, 32);                // R:G(b0-1)
-    VD_SP_FENCE();
-    mmaS(0);                      // M:S(b0) + the second half of V(b0-1)
-    softmax(1, 1);
-    sp_interleave<NMS, VD_SP_NV>();
-    VD_SP_FENCE();
-    readS(SG, 32);                // R:S(b1)
-    VD_SP_FENCE();
-    mmaG(1);                      // M:G(b0-1) + V(b0), first half
-    softmax(0, 0);
-    sp_interleave<NMG, VD_SP_NV>();
-    VD_SP_FENCE();
-    readG(SG, 0);                 // R:G(b0)
-    VD_SP_FENCE();
-    mmaS(1);                      // M:S(b1) + V(b0), second half
-    softmax(0, 1);
-    sp_interleave<NMS, VD_SP_NV>();
-    VD_SP_FENCE();
-  };
-  const int nt = (ntiles + NST - 1) / NST * NST;  // zero K / V tiles past the end add nothing
-  for (int t = 0; t < nt; t += NST) {
-    step(t, std::integral_constant<int, 0>{});
-    step(t + 1, std::integral_constant<int, 1>{});
-    step(t + 2, std::integral_constant<int, 2>{});
-    step(t + 3, std::integral_constant<int, 3>{});
-  }
-  softmax(1, 0);  // V(2nt-1), then G(2nt-2) (fragments already read), G(2nt-1)
-  softmax(1, 1);
-  mmaG(0);
-  readG((nt - 1) & (NST - 1), 32);
-  mmaG(1);
-  vm_drain();
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    f32x16 out[D / 32];
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i) out[i] = acc[i][j];
-    store_transposed<T, D / 32>(dq + base, ts, q0 + 32 * j + (lane & 31), n, 0, out, scale, lane);
-  }
-}
-
 // ------------------------------------------------------------------ launchers
 int check_attn(const vd_attn_desc* d) {
   VD_REQUIRE(d, "null descriptor");
@@ -2494,8 +1842,10 @@ int check_attn(const vd_attn_desc* d) {
 //   kRole: head_dim-256 dK/dV with role-split wave pairs (attn_bwd_dkdv_role_kernel)
 //   kP4N2: the pipelined backward kernels with 4 waves x 2 blocks (one wave per SIMD,
 //          each LDS fragment feeds two MFMAs; bf16, D = 64; fwd keeps its default)
-//   kSP: the fragment-pipelined backward kernels (attn_bwd_dq_sp_kernel /
-//          attn_bwd_dkdv_sp_kernel; bf16, D = 64, >= 16 key tiles; fwd keeps its default)
+//   kSP: retired (the fragment-pipelined backward measured equal to kP8, which it now
+//          selects; profiles/r02_ab_sp.txt)
+//   kAsm: the hand-scheduled head_dim-64 backward (asm/gen_attn_asm.py), one wave per SIMD
+//   kP8 / kP4 forward: retired (5 % slower than the deferred-check forward, which they select)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
                kPair = 8, kP4N2 = 9, kRole = 10, kSP = 11, kAsm = 12, kCfgLast = kAsm };
 
@@ -2653,21 +2003,6 @@ size_t fwd_ws_bytes(const vd_attn_desc* d, int nkv, bool cross) {
   return s > 1 ? (size_t)s * d->nseq * d->seq_len * (D + 2) * sizeof(float) : 0;
 }
 
-template <typename T, int D, int NW>
-int fwd_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
-                    float* lse, hipStream_t st) {
-  const size_t lds = tile_pipe_lds<D, false>();
-  auto kern = attn_fwd_pipe_kernel<T, D, NW>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW), (unsigned)d->nseq);
-  kern<<<grid, 64 * NW, lds, st>>>((const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
-                                   d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
-                                   d->token_stride,
-                                   SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
-                                   d->o_token_stride, d->scale);
-  return vd::check_launch("attn_fwd");
-}
 
 template <typename T, int D, int NW, bool STAGGER>
 int fwd_defer_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
@@ -2696,15 +2031,15 @@ int fwd_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const 
     if constexpr (D == 64 || D == 128)
       if (c == kW8) return fwd_launch<T, D, 1, 8>(d, kv, q, k, v, o, lse, nullptr, 0, st);
     if constexpr (D == 64) {
-      if (c == kP8) return fwd_pipe_launch<T, D, 8>(d, q, k, v, o, lse, st);
+      if (c == kP8) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
       if (c == kD8) return fwd_defer_launch<T, D, 8, true>(d, q, k, v, o, lse, st);
       if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
       if (c == kD4) return fwd_defer_launch<T, D, 4, false>(d, q, k, v, o, lse, st);
     }
     if constexpr (D == 128)
       if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
-    if constexpr (D <= 128)
-      if (c == kP4) return fwd_pipe_launch<T, D, 4>(d, q, k, v, o, lse, st);
+    if constexpr (D == 64 || D == 128)  // the pipelined forward is retired: its successor
+      if (c == kP4) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
   }
   return fwd_launch<T, D, 1, 4>(d, kv, q, k, v, o, lse, ws, ws_bytes, st);
 }
@@ -2755,51 +2090,6 @@ int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
                                    d->o_token_stride, d->scale);
   return vd::check_launch("attn_bwd_dq");
 }
-
-// fragment-pipelined backward (kSP): NW waves x NB x 32 rows per workgroup
-#ifndef VD_SP_NW
-#define VD_SP_NW 8
-#endif
-#ifndef VD_SP_NB
-#define VD_SP_NB 1
-#endif
-template <int D, int NW = VD_SP_NW, int NB = VD_SP_NB>
-int dq_sp_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                 const void* dout, const float* nlse2, const float* ndelta, void* dq,
-                 hipStream_t st) {
-  const size_t lds = tile_pipe_lds<D, false>();
-  auto kern = attn_bwd_dq_sp_kernel<D, NW, NB>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW * NB), (unsigned)d->nseq);
-  kern<<<grid, 64 * NW, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                               (const bf16_t*)dout, nlse2, ndelta, (bf16_t*)dq, d->seq_len,
-                               SeqAddr{d->batch_stride, d->group_stride, d->groups},
-                               d->token_stride,
-                               SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
-                               d->o_token_stride, d->scale);
-  return vd::check_launch("attn_bwd_dq");
-}
-template <int D, int NW = VD_SP_NW, int NB = VD_SP_NB>
-int dkdv_sp_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                   const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
-                   hipStream_t st) {
-  const size_t lds = tile_pipe_lds<D, true>();
-  auto kern = attn_bwd_dkdv_sp_kernel<D, NW, NB>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-  dim3 grid((unsigned)vd_cdiv(d->seq_len, 32 * NW * NB), (unsigned)d->nseq);
-  kern<<<grid, 64 * NW, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                               (const bf16_t*)dout, nlse2, ndelta, (bf16_t*)dk, (bf16_t*)dv,
-                               d->seq_len, SeqAddr{d->batch_stride, d->group_stride, d->groups},
-                               d->token_stride,
-                               SeqAddr{d->o_batch_stride, d->o_group_stride, d->groups},
-                               d->o_token_stride, d->scale);
-  return vd::check_launch("attn_bwd_dkdv");
-}
-// the fragment-pipelined kernels round the tile count up to the ring's 4 stages: shorter
-// sequences keep the 8-wave pipelines
-inline bool sp_ok(const vd_attn_desc* d) { return d->seq_len >= 16 * kTile; }
 
 // hand-scheduled head_dim-64 dQ (asm/gen_attn_asm.py): one wave per SIMD, 256 queries per
 // workgroup, tiles rounded up to the 4-stage ring; 32-bit buffer offsets of every row it
@@ -2889,8 +2179,6 @@ int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, con
       if (c == kNB2) return dq_launch<T, D, 2, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64 || D == 128)
       if (c == kW8) return dq_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
-    if constexpr (D == 64)
-      if (c == kSP && sp_ok(d)) return dq_sp_launch<D>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dq))
         return dq_asm_launch(d, q, k, v, dout, nlse2, ndelta, dq, st);
@@ -3020,9 +2308,6 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
       if (c == kNB2) return dkdv_launch<T, D, 2, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64 || D == 128)
       if (c == kW8) return dkdv_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
-    if constexpr (D == 64)
-      if (c == kSP && sp_ok(d))
-        return dkdv_sp_launch<D>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 64)
       if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dk) && asm_dq_ok(d, q, k, v, dout, dv))
         return dkdv_asm_launch(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
