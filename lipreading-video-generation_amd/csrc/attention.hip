@@ -1879,6 +1879,8 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //   D = 128: fwd NB2 2.0 ms, dQ W8 2.8 ms (P4 3.7), dK/dV base 4.7 ms (N = 65536); fwd D8N
   //            2.01 vs NB2 2.32-2.35 ms on the same box (tools/attn_ab.sh); dK/dV PAIR
   //            (round 2) 3.84-3.96 vs base 4.84-4.85 ms on the same box (tools/ab_d128.sh)
+  //   D = 64 backward (round 3): hand-scheduled dQ 18.8 / dK/dV 24.6 ms vs P8 20.8 / 28.9 ms
+  //            on the same box (tools/gpu_asm.sh)
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
@@ -1887,7 +1889,7 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kAsm && (D != 64 || kind == 0)) &&    // hand-scheduled: D = 64 backward
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
-  else if (D == 64) c = kind == 0 ? kD8N : kP8;
+  else if (D == 64) c = kind == 0 ? kD8N : kAsm;  // asm falls back to P8 off its shapes
   else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kPair);
   else if (D == 256 && kind == 2) c = kRole;
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;

@@ -66,7 +66,7 @@ def test_scores_with_large_logits():
 
 
 CONFIGS = ["auto", "base", "nb2", "w8", "p8", "p4", "d8", "d8n", "d4", "pair", "p4n2", "role",
-           "sp"]
+           "sp", "asm"]
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
@@ -128,7 +128,7 @@ def test_bf16_lagged_max_rescale_default_shapes(C):
 
 def test_config_hook_rejects_unknown():
     from vdiff import _lib, ops
-    assert _lib.lib().vd_attention_set_config(12) == -2
+    assert _lib.lib().vd_attention_set_config(13) == -2
     with pytest.raises(ValueError):
         ops.attention_config("fast")
 

@@ -1,5 +1,6 @@
 """The hand-scheduled head_dim-64 backward kernels (vd_attn_bwd_dq_d64 and
-vd_attn_bwd_dkdv_d64, csrc/asm/gen_attn_asm.py, attention config "asm") against the compiler-scheduled pipelined kernel (the default, config "auto") on the
+vd_attn_bwd_dkdv_d64, csrc/asm/gen_attn_asm.py, attention config "asm", the head_dim-64 backward default) against the compiler-scheduled
+pipelined kernels (config "p8", whose forward is the default deferred-check forward) on the
 same bf16 inputs, and against a materialised fp32 reference of QKVAttentionLegacy's backward
 (unet.py:349-366).  The asm kernel runs the same products in the same accumulation order,
 so dQ, dK and dV agree with the pipelined kernels' to fp32 rounding (bound 1e-6 rel-L2).
@@ -37,7 +38,7 @@ def _inputs(B, N, seed, spatial=None):
                                       (1, 65536 + 17, 4)])
 def test_asm_bwd_equals_pipelined_kernels(B, N, seed):
     qkv, g = _inputs(B, N, seed)
-    y0, g0 = _grads(qkv, g, "auto")
+    y0, g0 = _grads(qkv, g, "p8")
     y1, g1 = _grads(qkv, g, "asm")
     assert torch.equal(y0, y1)                     # the forward is not affected
     assert torch.isfinite(g1.float()).all()
@@ -51,10 +52,17 @@ def test_asm_bwd_equals_pipelined_kernels(B, N, seed):
 def test_asm_bwd_spatial_groups():
     qkv, g = _inputs(1, None, 5, spatial=(4, 32, 32))
     kw = dict(mode="spatial", spatial=(4, 32, 32))
-    _, g0 = _grads(qkv, g, "auto", **kw)
+    _, g0 = _grads(qkv, g, "p8", **kw)
     _, g1 = _grads(qkv, g, "asm", **kw)
     err = float((g0.float() - g1.float()).norm() / g0.float().norm())
     assert err <= 1e-6, err
+
+
+def test_asm_is_the_d64_backward_default():
+    qkv, g = _inputs(1, 2048, 7)
+    _, g0 = _grads(qkv, g, "auto")
+    _, g1 = _grads(qkv, g, "asm")
+    assert torch.equal(g0, g1)
 
 
 def test_asm_bwd_against_fp32_reference():

@@ -23,9 +23,13 @@ CALIB_WRITE = CALIB_ELEMS * 2
 
 _ATTN = re.compile(r"(attn_\w+?)_kernel<(?:[^,<>]+,\s*)?(\d+)")
 _VARIANT = re.compile(r"_(pipe|defer|pair)$")  # kernel variants share the launch's key
+_ASM = re.compile(r"^vd_(attn_\w+)_d(\d+)$")   # hand-scheduled kernels (asm/gen_attn_asm.py)
 
 
 def kernel_key(name: str) -> str:
+    m = _ASM.match(name)
+    if m:
+        return f"{m.group(1)}_d{m.group(2)}"
     m = _ATTN.search(name)
     if m:
         return f"{_VARIANT.sub('', m.group(1))}_d{m.group(2)}"
