@@ -480,13 +480,15 @@ def gen_dq(probe=None):
 
 def main():
     out = sys.argv[1]
+    from gen_fwd import gen_fwd
     kdq, ddq, sdq = gen_dq()
     kdk, ddk, sdk = gen_dkdv()
+    kfw, sfw = gen_fwd()
     with open(out, "w") as f:
         f.write("// generated by gen_attn_asm.py -- do not edit\n")
-        f.write(code_object_text([kdq, kdk], ddq + ddk))
+        f.write(code_object_text([kdq, kdk, kfw], ddq + ddk))
     if "--report" in sys.argv:
-        for name, st in (("dq", sdq), ("dkdv", sdk)):
+        for name, st in (("dq", sdq), ("dkdv", sdk), ("fwd", sfw)):
             print(f"{name}: {len(st.lines)} lines, {st.nops} nop wait states, {st.waits} lgkm "
                   f"waits, {st.forced} forced by the 15-read limit ({st.young} on young reads)")
 

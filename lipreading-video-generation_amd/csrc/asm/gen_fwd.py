@@ -1,0 +1,570 @@
+"""vd_attn_fwd_d64: hand-scheduled gfx950 forward of the head_dim-64 joint attention
+(reference QKVAttentionLegacy.forward, unet.py:349-366: softmax(Q K^T / sqrt(D)) V), the
+arithmetic of attn_fwd_defer_kernel<bf16, 64> in attention.hip laid out for ONE wave per
+SIMD: 4 waves x 64 queries (2 query blocks j) per workgroup, 256 queries per workgroup.
+
+Per 64-key tile t a wave runs 32 v_mfma_f32_32x32x16_bf16 in body t:
+    G(t-1, kb0) [8] | S(t+1, kb0) [8] | G(t-1, kb1) [8] | S(t+1, kb1) [8]
+with S^T = K Q'^T - m (the key on the accumulator rows, the query on the lane; srcC = the
+-m splat), G: O^T += V^T P^T (P^T as the B operand straight from the accumulators, the key
+permutation absorbed into the V^T transposed-read offsets as in the dQ kernel), and the
+softmax of tile t (64 v_exp_f32, 62 row-sum adds, 32 v_cvt_pk_bf16_f32) spread over the 32
+gaps of the same body by cost (exp 8 cycles, add 4, cvt 4.5).  S is computed one tile
+ahead into a second accumulator set, so the softmax stream never waits for its MFMAs.
+
+Lagged max (attention.hip kLagSum): p = exp2(S' - m) with the stale m; after the softmax of
+tile t the wave checks that every lane's tile sum is < 2^16 (false for inf / NaN too) and
+otherwise calls the rare path (a subroutine, s_swappc): recompute S(t) from the resident K
+tile, take the true row max over the tile (both lane halves), rescale O and l by
+exp2(m - m_new), redo tile t's softmax, and recompute S(t+1), whose MFMAs ran against the
+old m.  m starts at -inf (the -m splat at +inf), so the first tile always takes it.
+
+Ring: 8 stages x (K tile 8 KiB | V tile 8 KiB) = 128 KiB of LDS by LDS-DMA, tile t+4 issued
+in body t (4 pieces per wave spread over the body), one barrier per body behind
+s_waitcnt vmcnt(8).  The loop is unrolled by the 8 stages; keys past the end of the
+sequence (zero-filled by the buffer range check) are masked to -inf only in the last
+iteration, which is its own copy of the 8 bodies.
+"""
+from __future__ import annotations
+
+from asmgen import Regs, Stream, kernel_text
+
+MFMA = "v_mfma_f32_32x32x16_bf16"
+NW = 4
+NST = 8                # ring stages
+PD = 4                 # prefetch distance (tiles)
+STAGE = 16384          # K tile | V tile
+VOFF = 8192
+KARG = 112
+HI = 65536             # ds_read immediates are 16 bits: stages >= 4 use the +64 KiB bases
+NINF, PINF = "0xff800000", "0x7f800000"
+
+# kernel arguments (AsmFwdArgs in vd_asm.h), loaded into s[16:43]:
+#  0 q  8 k  16 v  24 o  32 lse                            (u64)   s16..s25
+#  40 n  44 ts_bytes  48 ots_bytes  52 groups              (u32)   s26..s29
+#  56 bs_bytes  64 gs_bytes  72 obs_bytes  80 ogs_bytes    (u64)   s30..s37
+#  88 qscale (f32)  92 kv_bytes  96 o_bytes  100 tile_bytes         s38..s41
+#  104 niter (512-key iterations, the last one masked)  108 klim0 (keys in it)  s42, s43
+S_KARG = "s[0:1]"
+S_WGX, S_WGY, S_WGZ = "s2", "s3", "s4"
+RQ, RK, RV, RO, RL = "s[44:47]", "s[48:51]", "s[52:55]", "s[56:59]", "s[60:63]"
+S_WAVE, S_Q0, S_M0, S_ITER, S_TAB = "s64", "s65", "s66", "s67", "s[68:69]"
+S_ST, S_ST1, S_KB, S_RET, S_TGT = "s76", "s77", "s78", "s[80:81]", 82
+
+
+def regs():
+    V, A = Regs("v"), Regs("a")
+    for name, n in (("tid", 1), ("lane", 1), ("rowoff", 4), ("troff", 4), ("rowhi", 4),
+                    ("trhi", 4), ("dma", 2), ("dmac", 2), ("tmp", 4), ("sto", 2), ("klim", 1),
+                    ("ps", 2), ("l", 2), ("m", 2), ("ninf", 1), ("tc", 2)):
+        V.alloc(name, n)
+    V.alloc("s0", 64, 16)    # S' of the even tiles, 4 slots p = 2 kb + j
+    V.alloc("s1", 64, 16)    # ... of the odd tiles
+    V.alloc("p", 32)         # P^T as bf16 B operands, 8 per slot
+    V.alloc("negm", 32)      # -m splats per query block (srcC of the first S MFMA)
+    A.alloc("qf", 32)        # Q' fragments [j][s]
+    A.alloc("acc", 64)       # O^T accumulators [i][j]
+    A.alloc("kf", 32)        # K row fragments [kb][s]
+    A.alloc("trf", 32)       # V^T fragments [kb][i][s2] (lo 2 + hi 2)
+    return V, A
+
+
+def sblk(V, par, p):
+    return V.r(f"s{par}", 16 * p, 16)
+
+
+def lds(V, base, off):
+    """(base register, immediate) of an LDS byte offset `off` from a per-lane table entry."""
+    if off >= HI:
+        return V.r({"rowoff": "rowhi", "troff": "trhi"}[base[0]], base[1]), off - HI
+    return V.r(base[0], base[1]), off
+
+
+def k_reads(V, A, stage, kb):
+    out = []
+    for s in range(4):
+        b, off = lds(V, ("rowoff", s), stage * STAGE + kb * 4096)
+        out.append((f"ds_read_b128 {A.r('kf', 16 * kb + 4 * s, 4)}, {b} offset:{off}",
+                    ("K", kb, s)))
+    return out
+
+
+def tr_reads(V, A, stage, kb):
+    out = []
+    for i in range(2):
+        for s2 in range(2):
+            for hi in range(2):
+                b, off = lds(V, ("troff", 2 * i + hi), stage * STAGE + VOFF + kb * 4096 + s2 * 2048)
+                out.append((f"ds_read_b64_tr_b16 {A.r('trf', 16 * kb + 8 * i + 4 * s2 + 2 * hi, 2)}"
+                            f", {b} offset:{off}", ("T", kb, i, s2, hi)))
+    return out
+
+
+def g_mfmas(V, A, kb):
+    out = []
+    for i in range(2):
+        for s2 in range(2):
+            tr = A.r("trf", 16 * kb + 8 * i + 4 * s2, 4)
+            for j in range(2):
+                acc = A.r("acc", 16 * (2 * i + j), 16)
+                pv = V.r("p", 8 * (2 * kb + j) + 4 * s2, 4)
+                out.append((f"{MFMA} {acc}, {tr}, {pv}, {acc}", ()))
+    return out
+
+
+def s_mfmas(V, A, par, kb, zero_c=False):
+    """S'(kb) of both query blocks into accumulator set `par` (srcC: -m, or 0)."""
+    out = []
+    for s in range(4):
+        for j in range(2):
+            d = sblk(V, par, 2 * kb + j)
+            c = ("0" if zero_c else V.r("negm", 16 * j, 16)) if s == 0 else d
+            out.append((f"{MFMA} {d}, {A.r('kf', 16 * kb + 4 * s, 4)}, "
+                        f"{A.r('qf', 16 * j + 4 * s, 4)}, {c}", (("K", kb, s),)))
+    return out
+
+
+# ------------------------------------------------------------------ softmax stream
+COST = {"exp": 8.0, "add": 4.0, "cvt": 4.5, "cmp": 4.0, "cnd": 4.0}
+
+
+def softmax_list(V, par, masked, u):
+    """The VALU of one tile's softmax: [(text, cost, earliest gap)].  A slot's bf16 P^T
+    is written only after G(t-1) of the same key block has read the previous tile's (gap 9 /
+    25); masked tiles set keys >= n to -inf first (klim = keys left - 4 hh)."""
+    out = []
+    for kb in range(2):
+        for j in range(2):
+            p = 2 * kb + j
+            S = V[f"s{par}"] + 16 * p
+            ps = V.r("ps", j)
+            if masked:
+                for r in range(16):
+                    c = 64 * u + 32 * kb + (r & 3) + 8 * (r >> 2)
+                    out.append((f"v_cmp_lt_i32 vcc, {c}, {V.r('klim')}", COST["cmp"], 0))
+                    out.append((f"v_cndmask_b32 v{S + r}, {V.r('ninf')}, v{S + r}, vcc",
+                                COST["cnd"], 0))
+            for k in range(8):
+                a, b = S + 2 * k, S + 2 * k + 1
+                out.append((f"v_exp_f32 v{a}, v{a}", COST["exp"], 0))
+                out.append((f"v_exp_f32 v{b}, v{b}", COST["exp"], 0))
+                if kb == 0 and k == 0:
+                    out.append((f"v_add_f32 {ps}, v{a}, v{b}", COST["add"], 0))
+                else:
+                    out.append((f"v_add_f32 {ps}, {ps}, v{a}", COST["add"], 0))
+                    out.append((f"v_add_f32 {ps}, {ps}, v{b}", COST["add"], 0))
+                out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + k)}, v{a}, v{b}", COST["cvt"],
+                            9 if kb == 0 else 25))
+    return out
+
+
+def place(items, ngaps):
+    """Greedy list schedule: gap g takes, in list order, the instructions whose earliest gap
+    has come, until the gap's share of the total cost is used; an instruction held back by
+    its earliest gap lets the later ones pass (only P^T writes are held back)."""
+    total = sum(c for _, c, _ in items)
+    per = total / ngaps
+    slots = [[] for _ in range(ngaps)]
+    done = [False] * len(items)
+    budget = 0.0
+    for g in range(ngaps):
+        budget += per
+        last = g == ngaps - 1
+        for k, (text, cost, early) in enumerate(items):
+            if done[k] or early > g:
+                continue
+            if not last and cost > budget + 1e-9:
+                break
+            slots[g].append(text)
+            budget -= cost
+            done[k] = True
+    assert all(done)
+    return slots
+
+
+# ------------------------------------------------------------------ prologue
+def prologue(st: Stream, V, A):
+    e, r = st.emit, st.raw
+    r(f"s_load_dwordx16 s[16:31], {S_KARG}, 0x0")
+    r(f"s_load_dwordx8 s[32:39], {S_KARG}, 0x40")
+    r(f"s_load_dwordx4 s[40:43], {S_KARG}, 0x60")
+    e(f"v_and_b32 {V.r('lane')}, 63, {V.r('tid')}")
+    r(f"v_readfirstlane_b32 {S_WAVE}, {V.r('tid')}")  # first lane's id = 64 * wave
+    r("s_nop 1")
+    r(f"s_lshr_b32 {S_WAVE}, {S_WAVE}, 6")
+    r("s_getpc_b64 s[68:69]")
+    r("s_add_u32 s68, s68, vd_attn_dq_lanes@rel32@lo+4")  # the dQ kernel's lane table
+    r("s_addc_u32 s69, s69, vd_attn_dq_lanes@rel32@hi+12")
+    # rare-path entry points: S_TGT + 2 v = .Lfwd_rare{v}
+    r(f"s_getpc_b64 s[{S_TGT}:{S_TGT + 1}]")
+    st.label(".Lfwd_pc")
+    for v in (3, 2, 1, 0):
+        r(f"s_add_u32 s{S_TGT + 2 * v}, s{S_TGT}, .Lfwd_rare{v}-.Lfwd_pc")
+        r(f"s_addc_u32 s{S_TGT + 2 * v + 1}, s{S_TGT + 1}, 0")
+    r("s_waitcnt lgkmcnt(0)")
+    # seq = wgz * groups + wgy ; base = wgz * bs + wgy * gs ; obase likewise (bytes, 64-bit)
+    r(f"s_mul_i32 s70, {S_WGZ}, s29")
+    r(f"s_add_u32 s70, s70, {S_WGY}")
+
+    def mad64(dlo, dhi, a, blo, bhi, t):
+        r(f"s_mul_i32 {dlo}, {a}, {blo}")
+        r(f"s_mul_hi_u32 {dhi}, {a}, {blo}")
+        r(f"s_mul_i32 {t}, {a}, {bhi}")
+        r(f"s_add_u32 {dhi}, {dhi}, {t}")
+
+    mad64("s72", "s73", S_WGZ, "s30", "s31", "s71")
+    mad64("s76", "s77", S_WGY, "s32", "s33", "s71")
+    r("s_add_u32 s72, s72, s76")
+    r("s_addc_u32 s73, s73, s77")
+    mad64("s74", "s75", S_WGZ, "s34", "s35", "s71")
+    mad64("s76", "s77", S_WGY, "s36", "s37", "s71")
+    r("s_add_u32 s74, s74, s76")
+    r("s_addc_u32 s75, s75, s77")
+
+    def rsrc(dst, plo, phi, blo, bhi, nrec):
+        d0 = int(dst[2:].split(":")[0])
+        r(f"s_add_u32 s{d0}, {plo}, {blo}")
+        r(f"s_addc_u32 s{d0 + 1}, {phi}, {bhi}")
+        r(f"s_and_b32 s{d0 + 1}, s{d0 + 1}, 0xffff")
+        r(f"s_mov_b32 s{d0 + 2}, {nrec}")
+        r(f"s_mov_b32 s{d0 + 3}, 0x20000")
+
+    rsrc(RQ, "s16", "s17", "s72", "s73", "s39")
+    rsrc(RK, "s18", "s19", "s72", "s73", "s39")
+    rsrc(RV, "s20", "s21", "s72", "s73", "s39")
+    rsrc(RO, "s22", "s23", "s74", "s75", "s40")
+    # lse row: seq * n * 4 bytes, n * 4 bytes long
+    r("s_mul_i32 s76, s70, s26")
+    r("s_mul_hi_u32 s77, s70, s26")
+    r("s_lshl_b64 s[76:77], s[76:77], 2")
+    r("s_lshl_b32 s71, s26, 2")
+    rsrc(RL, "s24", "s25", "s76", "s77", "s71")
+    # q0 = wgx * 256 + wave * 64 ; M0 base of this wave's DMA pieces = wave * 2048
+    r(f"s_lshl_b32 {S_Q0}, {S_WGX}, 8")
+    r(f"s_lshl_b32 s71, {S_WAVE}, 6")
+    r(f"s_add_u32 {S_Q0}, {S_Q0}, s71")
+    r(f"s_lshl_b32 {S_M0}, {S_WAVE}, 11")
+    r(f"s_sub_u32 {S_ITER}, s42, 1")
+    t0, t1 = V.r("tmp", 0), V.r("tmp", 1)
+    e(f"v_lshlrev_b32 {t0}, 6, {V.r('tid')}")
+    r(f"global_load_dwordx4 {V.r('rowoff', 0, 4)}, {t0}, {S_TAB}")
+    r(f"global_load_dwordx4 {V.r('troff', 0, 4)}, {t0}, {S_TAB} offset:16")
+    r(f"global_load_dwordx4 v[{V['dma']}:{V['dma'] + 3}], {t0}, {S_TAB} offset:32")
+    qrow = [V.r("s1", 60), V.r("s1", 61)]
+    hh16 = V.r("s1", 62)
+    e(f"v_and_b32 {qrow[0]}, 31, {V.r('lane')}")
+    e(f"v_add_u32 {qrow[0]}, {S_Q0}, {qrow[0]}")
+    e(f"v_add_u32 {qrow[1]}, 32, {qrow[0]}")
+    e(f"v_lshrrev_b32 {hh16}, 5, {V.r('lane')}")
+    e(f"v_lshlrev_b32 {hh16}, 4, {hh16}")
+    qv = V["s0"]  # Q fragments staged in v[s0 .. +31] for scaling
+    for j in range(2):
+        vq = V.r("s1", 56 + j)
+        e(f"v_mul_lo_u32 {vq}, {qrow[j]}, s27")
+        e(f"v_add_u32 {vq}, {vq}, {hh16}")
+        for s in range(4):
+            r(f"buffer_load_dwordx4 v[{qv + 16 * j + 4 * s}:{qv + 16 * j + 4 * s + 3}], {vq}, "
+              f"{RQ}, 0 offen offset:{32 * s}")
+        # O store offsets: qrow * ots_bytes + 8 hh
+        e(f"v_lshrrev_b32 {V.r('s1', 54)}, 1, {hh16}")
+        e(f"v_mul_lo_u32 {V.r('sto', j)}, {qrow[j]}, s28")
+        e(f"v_add_u32 {V.r('sto', j)}, {V.r('sto', j)}, {V.r('s1', 54)}")
+    # klim = keys in the last iteration - 4 hh
+    e(f"v_lshrrev_b32 {t1}, 2, {hh16}")
+    e(f"v_sub_u32 {V.r('klim')}, s43, {t1}")
+    r("s_waitcnt vmcnt(0)")
+    # Q' = bf16(Q * scale * log2 e), per bf16 element (attention.hip RowFrag::scale)
+    for w in range(32):
+        x = f"v{qv + w}"
+        e(f"v_lshlrev_b32 {t0}, 16, {x}")
+        e(f"v_and_b32 {t1}, 0xffff0000, {x}")
+        e(f"v_mul_f32 {t0}, s38, {t0}")
+        e(f"v_mul_f32 {t1}, s38, {t1}")
+        e(f"v_cvt_pk_bf16_f32 {x}, {t0}, {t1}")
+        e(f"v_accvgpr_write_b32 {A.r('qf', w)}, {x}")
+    for k in range(4):
+        e(f"v_add_u32 {V.r('rowhi', k)}, {HI:#x}, {V.r('rowoff', k)}")
+        e(f"v_add_u32 {V.r('trhi', k)}, {HI:#x}, {V.r('troff', k)}")
+    d0 = V["dma"]
+    for i in range(2):
+        e(f"v_mul_lo_u32 v{d0 + i}, v{d0 + i}, s27")
+        e(f"v_add_u32 v{d0 + i}, v{d0 + i}, v{d0 + 2 + i}")
+    # state: O = 0, l = 0, m = -inf (-m splat +inf), S'(0) = +inf (the first check fails),
+    # G(-1) adds 0 (zero V^T fragments and P^T)
+    for k in range(64):
+        e(f"v_accvgpr_write_b32 {A.r('acc', k)}, 0")
+    for k in range(32):
+        e(f"v_accvgpr_write_b32 {A.r('trf', k)}, 0")
+        e(f"v_mov_b32 {V.r('p', k)}, 0")
+        e(f"v_mov_b32 {V.r('negm', k)}, {PINF}")
+    for k in range(64):
+        e(f"v_mov_b32 {V.r('s0', k)}, {PINF}")
+    for j in range(2):
+        e(f"v_mov_b32 {V.r('m', j)}, {NINF}")
+        e(f"v_mov_b32 {V.r('l', j)}, 0")
+        e(f"v_mov_b32 {V.r('ps', j)}, 0")
+    e(f"v_mov_b32 {V.r('ninf')}, {NINF}")
+    for t in range(PD):
+        dma_tile(st, V, t)
+
+
+def dma_ops(V, stage):
+    d0 = V["dma"]
+    ops = []
+    for x, rs in ((0, RK), (VOFF, RV)):
+        for i in range(2):
+            ops.append((f"s_add_u32 m0, {S_M0}, {stage * STAGE + x + i * 1024}",
+                        f"buffer_load_dwordx4 v{d0 + i}, {rs}, 0 offen lds"))
+    adv = [f"v_add_u32 v{d0 + i}, s41, v{d0 + i}" for i in range(2)]
+    return ops, adv
+
+
+def dma_tile(st: Stream, V, stage):
+    ops, adv = dma_ops(V, stage)
+    for m0, ld in ops:
+        st.raw(m0)
+        st.raw("s_nop 0")
+        st.emit(ld)
+    for a in adv:
+        st.emit(a)
+
+
+# ------------------------------------------------------------------ one body
+def emit_body(st: Stream, V, A, u, masked, tag):
+    """Body of tile t (ring stage u = t mod 8): G(t-1), S(t+1), the softmax of tile t, the
+    lagged-max check of tile t."""
+    par = u % 2
+    st.comment(f"---- body, stage {u}{' (masked)' if masked else ''}")
+    st.raw(f"s_waitcnt vmcnt({(PD - 2) * 4}) lgkmcnt(0)")  # tile t+1 landed
+    st.raw("s_barrier")
+    st.flush_lds()
+    mf = g_mfmas(V, A, 0) + s_mfmas(V, A, 1 - par, 0) + g_mfmas(V, A, 1) + s_mfmas(V, A, 1 - par, 1)
+    nm = len(mf)
+    reads = {}
+
+    def put(slot0, lst, per=2):
+        for k, item in enumerate(lst):
+            reads.setdefault(slot0 + k // per, []).append(item)
+
+    kst = (u + 1) % NST
+    put(0, k_reads(V, A, kst, 0))      # K(t+1) rows, key block 0
+    put(8, tr_reads(V, A, u, 0))       # V(t)^T, for G(t) in the next body
+    put(16, k_reads(V, A, kst, 1))
+    put(24, tr_reads(V, A, u, 1))
+    ops, adv = dma_ops(V, (u + PD) % NST)
+    dma_at = {4: 0, 12: 1, 20: 2, 28: 3}
+    valu = place(softmax_list(V, par, masked, u), nm)
+    for g in range(nm):
+        if g in dma_at:
+            m0, ld = ops[dma_at[g]]
+            st.raw(m0)
+            st.raw("s_nop 0")
+            st.emit(ld)
+            if dma_at[g] == 3:
+                for a in adv:
+                    st.emit(a)
+        for text, rid in reads.get(g, []):
+            st.emit(text, lds_id=rid)
+        for text in valu[g]:
+            st.emit(text)
+        text, deps = mf[g]
+        st.emit(text, wait_lds=deps)
+    # lagged-max check of tile t: any lane's tile sum >= 2^16 (or inf / NaN) -> rare path
+    tc = V.r("tc", 0)
+    st.emit(f"v_max_f32 {tc}, {V.r('ps', 0)}, {V.r('ps', 1)}")
+    st.emit(f"v_cmp_ngt_f32 vcc, 0x47800000, {tc}")
+    st.raw("s_nop 3")
+    st.raw(f"s_cbranch_vccz .Lfwd_ok{tag}")
+    st.raw(f"s_mov_b32 {S_ST}, {u * STAGE}")
+    st.raw(f"s_mov_b32 {S_ST1}, {kst * STAGE}")
+    st.raw(f"s_mov_b32 {S_KB}, {64 * u}")
+    v = 2 * int(masked) + par
+    st.raw(f"s_swappc_b64 {S_RET}, s[{S_TGT + 2 * v}:{S_TGT + 2 * v + 1}]")
+    st.label(f".Lfwd_ok{tag}")
+    for j in range(2):
+        st.emit(f"v_add_f32 {V.r('l', j)}, {V.r('l', j)}, {V.r('ps', j)}")
+
+
+def emit_tail(st: Stream, V, A):
+    st.comment("---- tail: G of the last tile")
+    st.raw("s_waitcnt lgkmcnt(0)")
+    st.flush_lds()
+    for text, _ in g_mfmas(V, A, 0) + g_mfmas(V, A, 1):
+        st.emit(text)
+
+
+def epilogue(st: Stream, V, A):
+    e = st.emit
+    st.raw("s_waitcnt vmcnt(0)")
+    t = [V["s0"] + k for k in range(8)]
+    ad, lx, inv = V["s0"] + 8, V["s0"] + 10, V["s0"] + 12
+    e(f"v_xor_b32 v{ad}, 32, {V.r('lane')}")
+    e(f"v_lshlrev_b32 v{ad}, 2, v{ad}")
+    for j in range(2):
+        e(f"ds_bpermute_b32 v{lx + j}, v{ad}, {V.r('l', j)}")
+    st.raw("s_waitcnt lgkmcnt(0)")
+    for j in range(2):
+        e(f"v_add_f32 {V.r('l', j)}, {V.r('l', j)}, v{lx + j}")
+        e(f"v_rcp_f32 v{inv + j}, {V.r('l', j)}")
+    for j in range(2):
+        for i in range(2):
+            for g in range(4):
+                base = 16 * (2 * i + j) + 4 * g
+                for k in range(4):
+                    e(f"v_accvgpr_read_b32 v{t[k]}, {A.r('acc', base + k)}")
+                for k in range(4):
+                    e(f"v_mul_f32 v{t[k]}, v{inv + j}, v{t[k]}")
+                e(f"v_cvt_pk_bf16_f32 v{t[4]}, v{t[0]}, v{t[1]}")
+                e(f"v_cvt_pk_bf16_f32 v{t[5]}, v{t[2]}, v{t[3]}")
+                e(f"buffer_store_dwordx2 v[{t[4]}:{t[5]}], {V.r('sto', j)}, {RO}, 0 offen "
+                  f"offset:{64 * i + 16 * g}")
+    # lse = (m + log2 l) * ln 2 per query (both lane halves store the same value)
+    for j in range(2):
+        q, lg = V["s1"] + 2 * j, V["s1"] + 2 * j + 1
+        e(f"v_and_b32 v{q}, 31, {V.r('lane')}")
+        e(f"v_add_u32 v{q}, {S_Q0}, v{q}")
+        if j:
+            e(f"v_add_u32 v{q}, 32, v{q}")
+        e(f"v_lshlrev_b32 v{q}, 2, v{q}")
+        e(f"v_log_f32 v{lg}, {V.r('l', j)}")
+        e(f"v_add_f32 v{lg}, {V.r('m', j)}, v{lg}")
+        e(f"v_mul_f32 v{lg}, 0x3f317218, v{lg}")
+        e(f"buffer_store_dword v{lg}, v{q}, {RL}, 0 offen")
+
+
+# ------------------------------------------------------------------ the rare path
+def rare_path(V, A, par, masked):
+    """Subroutine .Lfwd_rare{2 masked + par}: S_ST / S_ST1 = ring offsets of tiles t / t+1,
+    S_KB = tile t's first key within the masked iteration; returns through S_RET."""
+    st = Stream()
+    e, r = st.emit, st.raw
+    st.label(f".Lfwd_rare{2 * int(masked) + par}")
+    r("s_nop 15")
+    r("s_nop 15")
+    r("s_waitcnt lgkmcnt(0)")
+    ta = [V.r("p", k) for k in range(4)]  # P^T is rewritten below: scratch until then
+
+    def reads_from(sreg):
+        for s in range(4):
+            e(f"v_add_u32 {ta[s]}, {sreg}, {V.r('rowoff', s)}")
+        for kb in range(2):
+            for s in range(4):
+                e(f"ds_read_b128 {A.r('kf', 16 * kb + 4 * s, 4)}, {ta[s]} offset:{kb * 4096}",
+                  lds_id=("K", kb, s))
+
+    reads_from(S_ST)
+    for kb in range(2):
+        for text, deps in s_mfmas(V, A, par, kb, zero_c=True):
+            e(text, wait_lds=deps)
+    st.flush_lds()
+    r("s_nop 15")
+    r("s_nop 15")
+    if masked:
+        vl = V.r("p", 4)
+        e(f"v_subrev_u32 {vl}, {S_KB}, {V.r('klim')}")
+        for kb in range(2):
+            for rr in range(16):
+                c = 32 * kb + (rr & 3) + 8 * (rr >> 2)
+                e(f"v_cmp_lt_i32 vcc, {c}, {vl}")
+                for j in range(2):
+                    x = V[f"s{par}"] + 16 * (2 * kb + j) + rr
+                    e(f"v_cndmask_b32 v{x}, {V.r('ninf')}, v{x}, vcc")
+    # true row max of tile t: 32 keys of the lane, then the other lane half
+    mx, oth, ad, alpha = V["p"] + 8, V["p"] + 10, V["p"] + 12, V["p"] + 14
+    for j in range(2):
+        R = [V[f"s{par}"] + 16 * (2 * kb + j) + k for kb in range(2) for k in range(16)]
+        e(f"v_max3_f32 v{mx + j}, v{R[0]}, v{R[1]}, v{R[2]}")
+        for k in range(3, 31, 2):
+            e(f"v_max3_f32 v{mx + j}, v{mx + j}, v{R[k]}, v{R[k + 1]}")
+        e(f"v_max_f32 v{mx + j}, v{mx + j}, v{R[31]}")
+    e(f"v_xor_b32 v{ad}, 32, {V.r('lane')}")
+    e(f"v_lshlrev_b32 v{ad}, 2, v{ad}")
+    for j in range(2):
+        e(f"ds_bpermute_b32 v{oth + j}, v{ad}, v{mx + j}")
+    r("s_waitcnt lgkmcnt(0)")
+    for j in range(2):
+        m, l = V.r("m", j), V.r("l", j)
+        e(f"v_max_f32 v{mx + j}, v{mx + j}, v{oth + j}")
+        e(f"v_max_f32 v{mx + j}, {m}, v{mx + j}")                 # m_new
+        e(f"v_sub_f32 v{alpha + j}, {m}, v{mx + j}")
+        e(f"v_exp_f32 v{alpha + j}, v{alpha + j}")               # exp2(m - m_new)
+        e(f"v_cmp_eq_f32 vcc, {m}, v{mx + j}")                    # equal (also -inf == -inf)
+        e(f"v_cndmask_b32 v{alpha + j}, v{alpha + j}, 1.0, vcc")
+        e(f"v_mov_b32 {m}, v{mx + j}")
+        e(f"v_mul_f32 {l}, v{alpha + j}, {l}")
+        e(f"v_xor_b32 v{oth + j}, 0x80000000, v{mx + j}")
+        for k in range(16):
+            e(f"v_mov_b32 {V.r('negm', 16 * j + k)}, v{oth + j}")
+        tmp = [V.r("tmp", k) for k in range(4)]
+        for i in range(2):
+            for g in range(4):
+                for k in range(4):
+                    e(f"v_accvgpr_read_b32 {tmp[k]}, {A.r('acc', 16 * (2 * i + j) + 4 * g + k)}")
+                for k in range(4):
+                    e(f"v_mul_f32 {tmp[k]}, v{alpha + j}, {tmp[k]}")
+                for k in range(4):
+                    e(f"v_accvgpr_write_b32 {A.r('acc', 16 * (2 * i + j) + 4 * g + k)}, {tmp[k]}")
+    # tile t's softmax against m_new (the m_new registers live in p[8..9], so slot 1's P^T
+    # words 0..1 are written after both query blocks' subtractions)
+    for j in range(2):
+        for kb in range(2):
+            S = V[f"s{par}"] + 16 * (2 * kb + j)
+            for k in range(16):
+                e(f"v_sub_f32 v{S + k}, v{S + k}, v{mx + j}")
+    for kb in range(2):
+        for j in range(2):
+            p = 2 * kb + j
+            S = V[f"s{par}"] + 16 * p
+            ps = V.r("ps", j)
+            for k in range(8):
+                a, b = S + 2 * k, S + 2 * k + 1
+                e(f"v_exp_f32 v{a}, v{a}")
+                e(f"v_exp_f32 v{b}, v{b}")
+                if kb == 0 and k == 0:
+                    e(f"v_add_f32 {ps}, v{a}, v{b}")
+                else:
+                    e(f"v_add_f32 {ps}, {ps}, v{a}")
+                    e(f"v_add_f32 {ps}, {ps}, v{b}")
+                e(f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + k)}, v{a}, v{b}")
+    # S(t+1) against m_new
+    ta = [V.r("tmp", k) for k in range(4)]
+    reads_from(S_ST1)
+    for kb in range(2):
+        for text, deps in s_mfmas(V, A, 1 - par, kb):
+            e(text, wait_lds=deps)
+    st.flush_lds()
+    r("s_nop 15")
+    r("s_nop 15")
+    r(f"s_setpc_b64 {S_RET}")
+    return st
+
+
+def gen_fwd(probe=None):
+    V, A = regs()
+    assert V.next <= 256 and A.next <= 256, (V.next, A.next)
+    st = Stream()
+    prologue(st, V, A)
+    if probe and probe[0] == "prologue":
+        from gen_attn_asm import emit_probe
+        emit_probe(st, probe[1], KARG, tmp=(V.r("tmp", 0), V.r("tmp", 1)))
+    st.label(".Lfwd_loop")
+    for u in range(NST):
+        emit_body(st, V, A, u, False, f"{u}")
+    st.raw(f"s_sub_u32 {S_ITER}, {S_ITER}, 1")
+    st.raw(f"s_cmp_lg_u32 {S_ITER}, 0")
+    st.raw("s_cbranch_scc1 .Lfwd_loop")
+    for u in range(NST):
+        emit_body(st, V, A, u, True, f"m{u}")
+    emit_tail(st, V, A)
+    if probe and probe[0] == "loop":
+        from gen_attn_asm import emit_probe
+        emit_probe(st, probe[1], KARG, tmp=(V.r("tmp", 0), V.r("tmp", 1)))
+    epilogue(st, V, A)
+    body = st.text() + "\ts_endpgm\n"
+    for masked in (False, True):
+        for par in range(2):
+            body += rare_path(V, A, par, masked).text()
+    k = kernel_text("vd_attn_fwd_d64", body, vgprs=V.next, agprs=A.next, sgprs=96,
+                    lds_bytes=NST * STAGE, kernarg_bytes=KARG + (8 if probe else 0),
+                    wg_size=64 * NW)
+    return k, st

@@ -1886,10 +1886,10 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
       !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
-      !(env == kAsm && (D != 64 || kind == 0)) &&    // hand-scheduled: D = 64 backward
+      !(env == kAsm && D != 64) &&                   // hand-scheduled: D = 64
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
-  else if (D == 64) c = kind == 0 ? kD8N : kAsm;  // asm falls back to P8 off its shapes
+  else if (D == 64) c = kAsm;  // falls back to D8N / P8 off its shapes
   else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kPair);
   else if (D == 256 && kind == 2) c = kRole;
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
@@ -2022,6 +2022,56 @@ int fwd_defer_launch(const vd_attn_desc* d, const void* q, const void* k, const 
   return vd::check_launch("attn_fwd");
 }
 
+// hand-scheduled head_dim-64 dQ (asm/gen_attn_asm.py): one wave per SIMD, 256 queries per
+// workgroup, tiles rounded up to the 4-stage ring; 32-bit buffer offsets of every row it
+// touches (the last DMA'd tiles run up to 5 tiles past the end), 16-B aligned rows
+inline bool asm_dq_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                      const void* dout, const void* dq) {
+  const int64_t n = d->seq_len;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return d->dtype == VD_BF16 && d->head_dim == 64 && n >= 16 * kTile && d->nseq % d->groups == 0 &&
+         d->token_stride % 8 == 0 && d->o_token_stride % 8 == 0 && d->token_stride >= 64 &&
+         d->o_token_stride >= 64 && d->batch_stride % 8 == 0 && d->group_stride % 8 == 0 &&
+         d->o_batch_stride % 8 == 0 && d->o_group_stride % 8 == 0 &&
+         (n + 512) * d->token_stride * 2 < 0x7fffffffLL &&
+         (n + 512) * d->o_token_stride * 2 < 0x7fffffffLL && al(q) && al(k) && al(v) &&
+         al(dout) && al(dq);
+}
+
+// hand-scheduled head_dim-64 forward (asm/gen_fwd.py): the dQ kernel's shape conditions
+// (the DMA runs up to 12 tiles past the end of the sequence: the 512-key rounding plus the
+// 4-tile prefetch) and a 4-byte aligned lse
+inline bool asm_fwd_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                       const void* o, const float* lse) {
+  const int64_t n = d->seq_len;
+  return asm_dq_ok(d, q, k, v, o, o) && (n + 1024) * d->token_stride * 2 < 0x7fffffffLL &&
+         ((uintptr_t)lse & 3) == 0;
+}
+
+int fwd_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
+                   float* lse, hipStream_t st) {
+  const int64_t n = d->seq_len;
+  vd::AsmFwdArgs a{};
+  a.q = q; a.k = k; a.v = v; a.o = o; a.lse = lse;
+  a.n = (uint32_t)n;
+  a.ts_bytes = (uint32_t)(d->token_stride * 2);
+  a.ots_bytes = (uint32_t)(d->o_token_stride * 2);
+  a.groups = (uint32_t)d->groups;
+  a.bs_bytes = (uint64_t)d->batch_stride * 2;
+  a.gs_bytes = (uint64_t)d->group_stride * 2;
+  a.obs_bytes = (uint64_t)d->o_batch_stride * 2;
+  a.ogs_bytes = (uint64_t)d->o_group_stride * 2;
+  a.qscale = d->scale * kLog2e;  // the fp32 product RowFrag::scale receives
+  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 64) * 2);
+  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 64) * 2);
+  a.tile_bytes = (uint32_t)(kTile * d->token_stride * 2);
+  a.niter = (uint32_t)vd_cdiv(n, 512);
+  a.klim0 = (uint32_t)(n - 512 * (int64_t)(a.niter - 1));
+  const int rc = vd::asm_fwd_d64(a, (unsigned)vd_cdiv(n, 256), (unsigned)d->groups,
+                                 (unsigned)(d->nseq / d->groups), st);
+  return rc ? rc : vd::check_launch("attn_fwd");
+}
+
 template <typename T, int D>
 int fwd_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
              const void* v, void* o, float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -2033,7 +2083,9 @@ int fwd_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const 
     if constexpr (D == 64 || D == 128)
       if (c == kW8) return fwd_launch<T, D, 1, 8>(d, kv, q, k, v, o, lse, nullptr, 0, st);
     if constexpr (D == 64) {
-      if (c == kP8) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
+      if (c == kAsm && asm_fwd_ok(d, q, k, v, o, lse))
+        return fwd_asm_launch(d, q, k, v, o, lse, st);
+      if (c == kP8 || c == kAsm) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
       if (c == kD8) return fwd_defer_launch<T, D, 8, true>(d, q, k, v, o, lse, st);
       if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
       if (c == kD4) return fwd_defer_launch<T, D, 4, false>(d, q, k, v, o, lse, st);
@@ -2091,22 +2143,6 @@ int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
                                    ndelta, (T*)dq, d->seq_len, qa, d->token_stride, oa,
                                    d->o_token_stride, d->scale);
   return vd::check_launch("attn_bwd_dq");
-}
-
-// hand-scheduled head_dim-64 dQ (asm/gen_attn_asm.py): one wave per SIMD, 256 queries per
-// workgroup, tiles rounded up to the 4-stage ring; 32-bit buffer offsets of every row it
-// touches (the last DMA'd tiles run up to 5 tiles past the end), 16-B aligned rows
-inline bool asm_dq_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                      const void* dout, const void* dq) {
-  const int64_t n = d->seq_len;
-  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  return d->dtype == VD_BF16 && d->head_dim == 64 && n >= 16 * kTile && d->nseq % d->groups == 0 &&
-         d->token_stride % 8 == 0 && d->o_token_stride % 8 == 0 && d->token_stride >= 64 &&
-         d->o_token_stride >= 64 && d->batch_stride % 8 == 0 && d->group_stride % 8 == 0 &&
-         d->o_batch_stride % 8 == 0 && d->o_group_stride % 8 == 0 &&
-         (n + 512) * d->token_stride * 2 < 0x7fffffffLL &&
-         (n + 512) * d->o_token_stride * 2 < 0x7fffffffLL && al(q) && al(k) && al(v) &&
-         al(dout) && al(dq);
 }
 
 int dq_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,

@@ -49,4 +49,22 @@ static_assert(sizeof(AsmDkdvArgs) == 144, "kernarg block layout");
 int asm_bwd_dkdv_d64(const AsmDkdvArgs& a, unsigned gx, unsigned gy, unsigned gz,
                      hipStream_t stream);
 
+// vd_attn_fwd_d64 kernarg block (asm/gen_fwd.py, 112 bytes): niter = 512-key iterations
+// (the last one masks keys >= n), klim0 = keys in the last iteration
+struct AsmFwdArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;
+  uint32_t n, ts_bytes, ots_bytes, groups;
+  uint64_t bs_bytes, gs_bytes, obs_bytes, ogs_bytes;
+  float qscale;
+  uint32_t kv_bytes, o_bytes, tile_bytes, niter, klim0;
+};
+static_assert(sizeof(AsmFwdArgs) == 112, "kernarg block layout");
+
+// grid (ceil(n / 256), groups, nseq / groups), 256 threads, 128 KiB static LDS
+int asm_fwd_d64(const AsmFwdArgs& a, unsigned gx, unsigned gy, unsigned gz, hipStream_t stream);
+
 }  // namespace vd

@@ -12,5 +12,5 @@ grep -E "PASS|FAIL|passed|failed|Error|error" gpurun_out/${TAG}_tests.log | tail
 for cfg in $CFGS; do
   echo "== cfg=$cfg"
   VDIFF_ATTN_CFG=$cfg timeout -k 10 150 python -u tools/attn_bench.py --nocheck 3 --only 64 \
-    2>&1 | tee -a gpurun_out/${TAG}_bench.log | grep -E "attn_bwd_dq|attn_bwd_dkdv"
+    2>&1 | tee -a gpurun_out/${TAG}_bench.log | grep -E "attn_fwd|attn_bwd_dq|attn_bwd_dkdv"
 done
