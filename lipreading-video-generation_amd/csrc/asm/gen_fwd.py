@@ -38,6 +38,13 @@ VOFF = 8192
 KARG = 112
 HI = 65536             # ds_read immediates are 16 bits: stages >= 4 use the +64 KiB bases
 NINF, PINF = "0xff800000", "0x7f800000"
+BAR2 = False           # A/B (tools/asm_ab.py): one barrier per two bodies
+CHECK_NOP = 3          # wait states between the check's v_cmp and its branch
+DROP = 0               # timing experiments only (wrong results): 1 exp, 2 add, 4 cvt, 8 reads
+CHAINS = 4             # row-sum accumulators per query block (1: one dependent add chain)
+NORARE = 0             # timing experiment only: never take the rare path (wrong results)
+STAMP = 0              # diagnostic: store loop cycles / realtime per workgroup (karg 112)
+GSGS = 0               # MFMA order of a body: 0 G(kb0) G(kb1) S(kb0) S(kb1); 1 G S G S
 
 # kernel arguments (AsmFwdArgs in vd_asm.h), loaded into s[16:43]:
 #  0 q  8 k  16 v  24 o  32 lse                            (u64)   s16..s25
@@ -56,7 +63,7 @@ def regs():
     V, A = Regs("v"), Regs("a")
     for name, n in (("tid", 1), ("lane", 1), ("rowoff", 4), ("troff", 4), ("rowhi", 4),
                     ("trhi", 4), ("dma", 2), ("dmac", 2), ("tmp", 4), ("sto", 2), ("klim", 1),
-                    ("ps", 2), ("l", 2), ("m", 2), ("ninf", 1), ("tc", 2)):
+                    ("ps", 2), ("l", 2), ("m", 2), ("ninf", 1), ("tc", 2), ("c", 8)):
         V.alloc(name, n)
     V.alloc("s0", 64, 16)    # S' of the even tiles, 4 slots p = 2 kb + j
     V.alloc("s1", 64, 16)    # ... of the odd tiles
@@ -129,32 +136,82 @@ COST = {"exp": 8.0, "add": 4.0, "cvt": 4.5, "cmp": 4.0, "cnd": 4.0}
 
 
 def softmax_list(V, par, masked, u):
-    """The VALU of one tile's softmax: [(text, cost, earliest gap)].  A slot's bf16 P^T
-    is written only after G(t-1) of the same key block has read the previous tile's (gap 9 /
-    25); masked tiles set keys >= n to -inf first (klim = keys left - 4 hh)."""
+    """The VALU of one tile's softmax: [(text, cost, earliest gap)] in issue order.  Per
+    score: v_exp_f32, an add into one of CHAINS row-sum accumulators of its query block
+    (round robin, 4 scores behind its exp, so neither the exp result nor the accumulator's
+    previous add is waited for), half a v_cvt_pk_bf16_f32.  A slot's bf16 P^T is written
+    only after G(t-1) of the same key block has read the previous tile's (earliest gap).
+    Masked tiles set keys >= n to -inf first (klim = keys left - 4 hh)."""
+    kinds = {"v_exp_f32": 1, "v_add_f32": 2, "v_mov_b32": 2, "v_cvt_pk_bf16_f32": 4}
+    gk = {0: 9, 1: 25} if GSGS else {0: 9, 1: 17}
     out = []
+    if CHAINS == 1:
+        for kb in range(2):
+            for j in range(2):
+                p = 2 * kb + j
+                S = V[f"s{par}"] + 16 * p
+                ps = V.r("ps", j)
+                out += mask_list(V, S, masked, u, kb)
+                for k in range(8):
+                    a, b = S + 2 * k, S + 2 * k + 1
+                    out.append((f"v_exp_f32 v{a}, v{a}", COST["exp"], 0))
+                    out.append((f"v_exp_f32 v{b}, v{b}", COST["exp"], 0))
+                    if kb == 0 and k == 0:
+                        out.append((f"v_add_f32 {ps}, v{a}, v{b}", COST["add"], 0))
+                    else:
+                        out.append((f"v_add_f32 {ps}, {ps}, v{a}", COST["add"], 0))
+                        out.append((f"v_add_f32 {ps}, {ps}, v{b}", COST["add"], 0))
+                    out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + k)}, v{a}, v{b}",
+                                COST["cvt"], gk[kb]))
+        return [it for it in out if not DROP & kinds.get(it[0].split()[0], 0)]
+    # the tile's 64 scores in slot order; E = exp, A = accumulate (4 scores behind), C = cvt
+    seq = []
     for kb in range(2):
         for j in range(2):
+            for r in range(16):
+                seq.append((kb, j, r))
+    lag = 4
+    for i in range(len(seq) + lag):
+        if i < len(seq):
+            kb, j, r = seq[i]
             p = 2 * kb + j
             S = V[f"s{par}"] + 16 * p
-            ps = V.r("ps", j)
-            if masked:
-                for r in range(16):
-                    c = 64 * u + 32 * kb + (r & 3) + 8 * (r >> 2)
-                    out.append((f"v_cmp_lt_i32 vcc, {c}, {V.r('klim')}", COST["cmp"], 0))
-                    out.append((f"v_cndmask_b32 v{S + r}, {V.r('ninf')}, v{S + r}, vcc",
-                                COST["cnd"], 0))
-            for k in range(8):
-                a, b = S + 2 * k, S + 2 * k + 1
-                out.append((f"v_exp_f32 v{a}, v{a}", COST["exp"], 0))
-                out.append((f"v_exp_f32 v{b}, v{b}", COST["exp"], 0))
-                if kb == 0 and k == 0:
-                    out.append((f"v_add_f32 {ps}, v{a}, v{b}", COST["add"], 0))
-                else:
-                    out.append((f"v_add_f32 {ps}, {ps}, v{a}", COST["add"], 0))
-                    out.append((f"v_add_f32 {ps}, {ps}, v{b}", COST["add"], 0))
-                out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + k)}, v{a}, v{b}", COST["cvt"],
-                            9 if kb == 0 else 25))
+            if r == 0:
+                out += mask_list(V, S, masked, u, kb)
+            out.append((f"v_exp_f32 v{S + r}, v{S + r}", COST["exp"], 0))
+        if i >= lag:
+            kb, j, r = seq[i - lag]
+            p = 2 * kb + j
+            S = V[f"s{par}"] + 16 * p
+            c = V.r("c", 4 * j + r % CHAINS)
+            if kb == 0 and r < CHAINS:
+                out.append((f"v_mov_b32 {c}, v{S + r}", COST["add"], 0))
+            else:
+                out.append((f"v_add_f32 {c}, {c}, v{S + r}", COST["add"], 0))
+            if r % 2:
+                k = r // 2
+                out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + k)}, v{S + r - 1}, v{S + r}",
+                            COST["cvt"], gk[kb]))
+    # combine the accumulators of each query block into ps
+    for j in range(2):
+        out.append((f"v_add_f32 {V.r('c', 4 * j)}, {V.r('c', 4 * j)}, {V.r('c', 4 * j + 1)}",
+                    COST["add"], 0))
+    for j in range(2):
+        out.append((f"v_add_f32 {V.r('c', 4 * j + 2)}, {V.r('c', 4 * j + 2)}, "
+                    f"{V.r('c', 4 * j + 3)}", COST["add"], 0))
+    for j in range(2):
+        out.append((f"v_add_f32 {V.r('ps', j)}, {V.r('c', 4 * j)}, {V.r('c', 4 * j + 2)}",
+                    COST["add"], 0))
+    return [it for it in out if not DROP & kinds.get(it[0].split()[0], 0)]
+
+
+def mask_list(V, S, masked, u, kb):
+    out = []
+    if masked:
+        for r in range(16):
+            c = 64 * u + 32 * kb + (r & 3) + 8 * (r >> 2)
+            out.append((f"v_cmp_lt_i32 vcc, {c}, {V.r('klim')}", COST["cmp"], 0))
+            out.append((f"v_cndmask_b32 v{S + r}, {V.r('ninf')}, v{S + r}, vcc", COST["cnd"], 0))
     return out
 
 
@@ -245,6 +302,7 @@ def prologue(st: Stream, V, A):
     r(f"s_add_u32 {S_Q0}, {S_Q0}, s71")
     r(f"s_lshl_b32 {S_M0}, {S_WAVE}, 11")
     r(f"s_sub_u32 {S_ITER}, s42, 1")
+    r("s_mov_b32 s79, 0")
     t0, t1 = V.r("tmp", 0), V.r("tmp", 1)
     e(f"v_lshlrev_b32 {t0}, 6, {V.r('tid')}")
     r(f"global_load_dwordx4 {V.r('rowoff', 0, 4)}, {t0}, {S_TAB}")
@@ -335,10 +393,23 @@ def emit_body(st: Stream, V, A, u, masked, tag):
     lagged-max check of tile t."""
     par = u % 2
     st.comment(f"---- body, stage {u}{' (masked)' if masked else ''}")
-    st.raw(f"s_waitcnt vmcnt({(PD - 2) * 4}) lgkmcnt(0)")  # tile t+1 landed
-    st.raw("s_barrier")
+    if not BAR2:
+        st.raw(f"s_waitcnt vmcnt({(PD - 2) * 4}) lgkmcnt(0)")  # tile t+1 landed
+        st.raw("s_barrier")
+    elif u % 2 == 0:
+        st.raw(f"s_waitcnt vmcnt({(PD - 3) * 4}) lgkmcnt(0)")  # tiles t+1, t+2 landed
+        st.raw("s_barrier")
+    else:
+        st.raw("s_waitcnt lgkmcnt(0)")
     st.flush_lds()
-    mf = g_mfmas(V, A, 0) + s_mfmas(V, A, 1 - par, 0) + g_mfmas(V, A, 1) + s_mfmas(V, A, 1 - par, 1)
+    if GSGS:
+        mf = (g_mfmas(V, A, 0) + s_mfmas(V, A, 1 - par, 0) + g_mfmas(V, A, 1)
+              + s_mfmas(V, A, 1 - par, 1))
+        rslots = (0, 8, 16, 24)
+    else:
+        mf = (g_mfmas(V, A, 0) + g_mfmas(V, A, 1) + s_mfmas(V, A, 1 - par, 0)
+              + s_mfmas(V, A, 1 - par, 1))
+        rslots = (2, 8, 12, 16)
     nm = len(mf)
     reads = {}
 
@@ -347,10 +418,11 @@ def emit_body(st: Stream, V, A, u, masked, tag):
             reads.setdefault(slot0 + k // per, []).append(item)
 
     kst = (u + 1) % NST
-    put(0, k_reads(V, A, kst, 0))      # K(t+1) rows, key block 0
-    put(8, tr_reads(V, A, u, 0))       # V(t)^T, for G(t) in the next body
-    put(16, k_reads(V, A, kst, 1))
-    put(24, tr_reads(V, A, u, 1))
+    if not DROP & 8:
+        put(rslots[0], k_reads(V, A, kst, 0))  # K(t+1) rows, key block 0
+        put(rslots[1], tr_reads(V, A, u, 0))   # V(t)^T, for G(t) in the next body
+        put(rslots[2], k_reads(V, A, kst, 1))
+        put(rslots[3], tr_reads(V, A, u, 1))
     ops, adv = dma_ops(V, (u + PD) % NST)
     dma_at = {4: 0, 12: 1, 20: 2, 28: 3}
     valu = place(softmax_list(V, par, masked, u), nm)
@@ -373,8 +445,11 @@ def emit_body(st: Stream, V, A, u, masked, tag):
     tc = V.r("tc", 0)
     st.emit(f"v_max_f32 {tc}, {V.r('ps', 0)}, {V.r('ps', 1)}")
     st.emit(f"v_cmp_ngt_f32 vcc, 0x47800000, {tc}")
-    st.raw("s_nop 3")
+    if CHECK_NOP:
+        st.raw(f"s_nop {CHECK_NOP}")
     st.raw(f"s_cbranch_vccz .Lfwd_ok{tag}")
+    if NORARE:
+        st.raw(f"s_branch .Lfwd_ok{tag}")
     st.raw(f"s_mov_b32 {S_ST}, {u * STAGE}")
     st.raw(f"s_mov_b32 {S_ST1}, {kst * STAGE}")
     st.raw(f"s_mov_b32 {S_KB}, {64 * u}")
@@ -439,6 +514,7 @@ def rare_path(V, A, par, masked):
     st = Stream()
     e, r = st.emit, st.raw
     st.label(f".Lfwd_rare{2 * int(masked) + par}")
+    r("s_add_u32 s79, s79, 1")  # rare-path count (read by diagnostic probes only)
     r("s_nop 15")
     r("s_nop 15")
     r("s_waitcnt lgkmcnt(0)")
@@ -539,6 +615,30 @@ def rare_path(V, A, par, masked):
     return st
 
 
+def emit_stamp(st: Stream, V):
+    """STAMP builds: lane 0 of each wave stores (loop cycles, loop realtime ticks) at
+    dbg[(wgx * 4 + wave) * 2] (dbg pointer at kernarg offset KARG)."""
+    r = st.raw
+    r("s_memtime s[94:95]")
+    r("s_memrealtime s[72:73]")
+    r(f"s_load_dwordx2 s[74:75], {S_KARG}, {KARG}")
+    r("s_waitcnt lgkmcnt(0)")
+    r("s_sub_u32 s94, s94, s90")
+    r("s_sub_u32 s72, s72, s92")
+    t0, t1, t2 = V.r("tmp", 0), V.r("tmp", 1), V.r("tmp", 2)
+    r(f"s_lshl_b32 s70, {S_WGX}, 2")
+    r(f"s_add_u32 s70, s70, {S_WAVE}")
+    r("s_lshl_b32 s70, s70, 3")
+    r(f"v_mov_b32 {t0}, s70")
+    r(f"v_mov_b32 {t1}, s94")
+    r(f"v_mov_b32 {t2}, s72")
+    r("s_mov_b64 exec, 1")
+    r(f"global_store_dword {t0}, {t1}, s[74:75]")
+    r(f"global_store_dword {t0}, {t2}, s[74:75] offset:4")
+    r("s_mov_b64 exec, -1")
+    r("s_waitcnt vmcnt(0)")
+
+
 def gen_fwd(probe=None):
     V, A = regs()
     assert V.next <= 256 and A.next <= 256, (V.next, A.next)
@@ -547,6 +647,9 @@ def gen_fwd(probe=None):
     if probe and probe[0] == "prologue":
         from gen_attn_asm import emit_probe
         emit_probe(st, probe[1], KARG, tmp=(V.r("tmp", 0), V.r("tmp", 1)))
+    if STAMP:
+        st.raw("s_memtime s[90:91]")
+        st.raw("s_memrealtime s[92:93]")
     st.label(".Lfwd_loop")
     for u in range(NST):
         emit_body(st, V, A, u, False, f"{u}")
@@ -556,6 +659,8 @@ def gen_fwd(probe=None):
     for u in range(NST):
         emit_body(st, V, A, u, True, f"m{u}")
     emit_tail(st, V, A)
+    if STAMP:
+        emit_stamp(st, V)
     if probe and probe[0] == "loop":
         from gen_attn_asm import emit_probe
         emit_probe(st, probe[1], KARG, tmp=(V.r("tmp", 0), V.r("tmp", 1)))
@@ -565,6 +670,6 @@ def gen_fwd(probe=None):
         for par in range(2):
             body += rare_path(V, A, par, masked).text()
     k = kernel_text("vd_attn_fwd_d64", body, vgprs=V.next, agprs=A.next, sgprs=96,
-                    lds_bytes=NST * STAGE, kernarg_bytes=KARG + (8 if probe else 0),
+                    lds_bytes=NST * STAGE, kernarg_bytes=KARG + (8 if probe or STAMP else 0),
                     wg_size=64 * NW)
     return k, st
