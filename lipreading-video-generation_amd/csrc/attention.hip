@@ -1886,7 +1886,8 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
       !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
-      !(env == kAsm && D != 64) &&                   // hand-scheduled: D = 64
+      !(env == kAsm && D != 64 && !(D == 128 && kind != 0)) &&  // hand-scheduled: D = 64,
+                                                     // D = 128 backward
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kAsm;  // falls back to D8N / P8 off its shapes
@@ -2026,12 +2027,12 @@ int fwd_defer_launch(const vd_attn_desc* d, const void* q, const void* k, const 
 // workgroup, tiles rounded up to the 4-stage ring; 32-bit buffer offsets of every row it
 // touches (the last DMA'd tiles run up to 5 tiles past the end), 16-B aligned rows
 inline bool asm_dq_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                      const void* dout, const void* dq) {
+                      const void* dout, const void* dq, int D = 64) {
   const int64_t n = d->seq_len;
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  return d->dtype == VD_BF16 && d->head_dim == 64 && n >= 16 * kTile && d->nseq % d->groups == 0 &&
-         d->token_stride % 8 == 0 && d->o_token_stride % 8 == 0 && d->token_stride >= 64 &&
-         d->o_token_stride >= 64 && d->batch_stride % 8 == 0 && d->group_stride % 8 == 0 &&
+  return d->dtype == VD_BF16 && d->head_dim == D && n >= 16 * kTile && d->nseq % d->groups == 0 &&
+         d->token_stride % 8 == 0 && d->o_token_stride % 8 == 0 && d->token_stride >= D &&
+         d->o_token_stride >= D && d->batch_stride % 8 == 0 && d->group_stride % 8 == 0 &&
          d->o_batch_stride % 8 == 0 && d->o_group_stride % 8 == 0 &&
          (n + 512) * d->token_stride * 2 < 0x7fffffffLL &&
          (n + 512) * d->o_token_stride * 2 < 0x7fffffffLL && al(q) && al(k) && al(v) &&
@@ -2145,10 +2146,12 @@ int dq_pipe_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
   return vd::check_launch("attn_bwd_dq");
 }
 
+// hand-scheduled dQ: head_dim 64 (256 queries per workgroup) or 128 (asm/gen_d128.py, 128)
 int dq_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                   const void* dout, const float* nlse2, const float* ndelta, void* dq,
                   hipStream_t st) {
   const int64_t n = d->seq_len;
+  const int D = d->head_dim;
   vd::AsmDqArgs a{};
   a.q = q; a.k = k; a.v = v; a.dout = dout; a.nlse2 = nlse2; a.ndelta = ndelta; a.dq = dq;
   a.n = (uint32_t)n;
@@ -2161,18 +2164,21 @@ int dq_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const voi
   a.ogs_bytes = (uint64_t)d->o_group_stride * 2;
   a.scale = d->scale;
   a.qscale = d->scale * kLog2e;  // the fp32 product RowFrag::scale receives
-  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 64) * 2);
-  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 64) * 2);
+  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + D) * 2);
+  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + D) * 2);
   a.tile_bytes = (uint32_t)(kTile * d->token_stride * 2);
   a.niter = (uint32_t)vd_cdiv(vd_cdiv(n, kTile), 4);
-  const int rc = vd::asm_bwd_dq_d64(a, (unsigned)vd_cdiv(n, 256), (unsigned)d->groups,
-                                    (unsigned)(d->nseq / d->groups), st);
+  const unsigned gy = (unsigned)d->groups, gz = (unsigned)(d->nseq / d->groups);
+  const int rc = D == 128 ? vd::asm_bwd_dq_d128(a, (unsigned)vd_cdiv(n, 128), gy, gz, st)
+                          : vd::asm_bwd_dq_d64(a, (unsigned)vd_cdiv(n, 256), gy, gz, st);
   return rc ? rc : vd::check_launch("attn_bwd_dq");
 }
 
+// hand-scheduled dK/dV: head_dim 64 (256 keys per workgroup) or 128 (asm/gen_d128.py, 128)
 int dkdv_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                     const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
                     hipStream_t st) {
+  const int D = d->head_dim;
   const int64_t n = d->seq_len;
   vd::AsmDkdvArgs a{};
   a.q = q; a.k = k; a.v = v; a.dout = dout; a.nlse2 = nlse2; a.ndelta = ndelta;
@@ -2187,13 +2193,14 @@ int dkdv_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const v
   a.ogs_bytes = (uint64_t)d->o_group_stride * 2;
   a.scale = d->scale;
   a.kscale = d->scale * kLog2e;
-  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 64) * 2);
-  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 64) * 2);
+  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + D) * 2);
+  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + D) * 2);
   a.tile_bytes = (uint32_t)(kTile * d->token_stride * 2);
   a.otile_bytes = (uint32_t)(kTile * d->o_token_stride * 2);
   a.niter = (uint32_t)vd_cdiv(vd_cdiv(n, kTile), 4);
-  const int rc = vd::asm_bwd_dkdv_d64(a, (unsigned)vd_cdiv(n, 256), (unsigned)d->groups,
-                                      (unsigned)(d->nseq / d->groups), st);
+  const unsigned gy = (unsigned)d->groups, gz = (unsigned)(d->nseq / d->groups);
+  const int rc = D == 128 ? vd::asm_bwd_dkdv_d128(a, (unsigned)vd_cdiv(n, 128), gy, gz, st)
+                          : vd::asm_bwd_dkdv_d64(a, (unsigned)vd_cdiv(n, 256), gy, gz, st);
   return rc ? rc : vd::check_launch("attn_bwd_dkdv");
 }
 
@@ -2215,8 +2222,12 @@ int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, con
     const AttnCfg c = pick_cfg(D, true, 1);
     if constexpr (D != 256)
       if (c == kNB2) return dq_launch<T, D, 2, 4>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D == 128)
+      if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dq, D))
+        return dq_asm_launch(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64 || D == 128)
-      if (c == kW8) return dq_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
+      if (c == kW8 || (D == 128 && c == kAsm))
+        return dq_launch<T, D, 1, 8>(d, kv, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D == 64)
       if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dq))
         return dq_asm_launch(d, q, k, v, dout, nlse2, ndelta, dq, st);
@@ -2358,7 +2369,11 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
     if constexpr (D <= 128)
       if (c == kP4) return dkdv_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 128)
-      if (c == kPair) return dkdv_pair_launch<D>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+      if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dk, D) && asm_dq_ok(d, q, k, v, dout, dv, D))
+        return dkdv_asm_launch(d, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 128)
+      if (c == kPair || c == kAsm)
+        return dkdv_pair_launch<D>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
     if constexpr (D == 256)
       if (c == kRole) {
         const BwdWs w = bwd_ws<D>(d, kv.n, cross);

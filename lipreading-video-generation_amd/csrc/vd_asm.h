@@ -49,6 +49,16 @@ static_assert(sizeof(AsmDkdvArgs) == 144, "kernarg block layout");
 int asm_bwd_dkdv_d64(const AsmDkdvArgs& a, unsigned gx, unsigned gy, unsigned gz,
                      hipStream_t stream);
 
+// vd_attn_bwd_dq_d128 (asm/gen_d128.py): the dQ kernarg block; grid (ceil(n / 128), groups,
+// nseq / groups), 256 threads, 128 KiB static LDS
+int asm_bwd_dq_d128(const AsmDqArgs& a, unsigned gx, unsigned gy, unsigned gz,
+                    hipStream_t stream);
+
+// vd_attn_bwd_dkdv_d128 (asm/gen_d128.py): the same kernarg block; grid (ceil(n / 128),
+// groups, nseq / groups), 256 threads, 131 KiB static LDS
+int asm_bwd_dkdv_d128(const AsmDkdvArgs& a, unsigned gx, unsigned gy, unsigned gz,
+                      hipStream_t stream);
+
 // vd_attn_fwd_d64 kernarg block (asm/gen_fwd.py, 112 bytes): niter = 512-key iterations
 // (the last one masks keys >= n), klim0 = keys in the last iteration
 struct AsmFwdArgs {
