@@ -213,6 +213,19 @@ int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dty
                     float* out, void* workspace, void* stream);
 int vd_conv_pack_weight(const float* w, int Co, int Ci, int taps, int Cip, int Cop,
                         int transpose, int dtype, void* out, void* stream);
+/* vd_conv_pack_weights: n vd_conv_pack_weight jobs in ONE launch (a training step's conv
+ * operands, re-packed once per optimizer step -- the weights that train.py:128-134's
+ * optimizer.step() just updated).  `descs` is a DEVICE array of n descriptors with
+ * start = the job's first element in the concatenation of all outputs (ascending, start[0]
+ * = 0) and `total` the concatenation's length; every output is in `dtype`.  n <= 1024. */
+typedef struct {
+  const float* w;
+  void* out;
+  int Co, Ci, taps, Cip, Cop, transpose;
+  int64_t start;
+} vd_pack_desc;
+int vd_conv_pack_weights(const vd_pack_desc* descs, int n, int64_t total, int dtype,
+                         void* stream);
 
 /* ---- Flash attention --------------------------------------------------
  * replaces QKVAttentionLegacy.forward (unet.py:349-366) + the fp32 softmax

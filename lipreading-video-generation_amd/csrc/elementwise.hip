@@ -342,6 +342,38 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int Co, int Ci, 
   }
 }
 
+// vd_conv_pack_weights: the jobs' outputs concatenated into one index space; each block
+// stages the jobs' start offsets in LDS and each element finds its job by binary search.
+template <typename T>
+__global__ void pack_weights_kernel(const vd_pack_desc* __restrict__ descs, int n,
+                                    int64_t total) {
+  __shared__ int64_t start[1024];
+  for (int j = threadIdx.x; j < n; j += blockDim.x) start[j] = descs[j].start;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {  // the last job whose start <= i
+      const int mid = (lo + hi + 1) >> 1;
+      if (start[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const vd_pack_desc& d = descs[lo];
+    const int64_t e = i - start[lo];
+    int co, ci, tap;
+    if (!d.transpose) {
+      ci = (int)(e % d.Cip);
+      tap = (int)((e / d.Cip) % d.taps);
+      co = (int)(e / ((int64_t)d.Cip * d.taps));
+    } else {
+      co = (int)(e % d.Cop);
+      tap = (int)((e / d.Cop) % d.taps);
+      ci = (int)(e / ((int64_t)d.Cop * d.taps));
+    }
+    const float v = (co < d.Co && ci < d.Ci) ? d.w[((int64_t)co * d.Ci + ci) * d.taps + tap] : 0.f;
+    Elem<T>::st((T*)d.out + e, v);
+  }
+}
+
 extern "C" {
 
 int vd_timestep_embedding(const int64_t* t, int B, int dim, float max_period, float* out,
@@ -478,6 +510,14 @@ int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dty
         (const Tp*)x, S, C, cs, rows, part);
     channel_sums_finish_kernel<<<dim3((unsigned)vd_cdiv(C, 32), (unsigned)B), 256, 0, st>>>(
         part, (int)blocks, C, out);
+  });
+}
+
+int vd_conv_pack_weights(const vd_pack_desc* descs, int n, int64_t total, int dtype,
+                         void* stream) {
+  VD_REQUIRE(descs && n > 0 && n <= 1024 && total > 0, "bad pack job list");
+  return VD_DISPATCH_DTYPE(dtype, Tp, {
+    pack_weights_kernel<Tp><<<grid_for(total), kBlock, 0, VD_STREAM(stream)>>>(descs, n, total);
   });
 }
 

@@ -10,6 +10,7 @@ Differences from the reference loops (all deliberate):
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass
@@ -68,10 +69,12 @@ class Trainer:
     train.py:102-103: Adam(model.parameters(), lr=1e-2), MSELoss."""
 
     def __init__(self, model, scheduler, lr=1e-2, bucket_mb=25.0, fused_adam=True,
-                 check_every=50):
+                 check_every=50, batch_pack=True):
         """check_every: the loss finiteness flag (kept on the device, updated every step) is
         read on the host every `check_every` steps and by check_finite(); a non-finite
-        loss raises FloatingPointError naming the first bad step.  0 disables it."""
+        loss raises FloatingPointError naming the first bad step.  0 disables it.
+        batch_pack: re-pack the conv operands once per step in one launch
+        (ops.step_packed_weights) instead of per conv call."""
         self.model = model
         self.scheduler = scheduler
         self.check_every = int(check_every)
@@ -84,13 +87,16 @@ class Trainer:
         self.bucketer = GradBucketer(params, bucket_mb) if distributed else None
         kw = {"fused": True} if fused_adam and params and params[0].is_cuda else {}
         self.opt = torch.optim.Adam(params, lr=lr, **kw)
+        # conv operands re-packed once per step in one launch (ops.step_packed_weights)
+        self.packs = ops.step_packed_weights() if batch_pack else contextlib.nullcontext()
 
     def step(self, clip: Clip) -> torch.Tensor:
         self.model.train()
-        xt = self.scheduler.add_noise(clip.x0, clip.eps, clip.t)
-        pred = self.model(xt, clip.cond, clip.audio, clip.t)
-        loss = F.mse_loss(pred, clip.eps)
-        loss.backward()
+        with self.packs:
+            xt = self.scheduler.add_noise(clip.x0, clip.eps, clip.t)
+            pred = self.model(xt, clip.cond, clip.audio, clip.t)
+            loss = F.mse_loss(pred, clip.eps)
+            loss.backward()
         if self.bucketer is not None:
             self.bucketer.finish()
             self.bucketer.step(self.opt)

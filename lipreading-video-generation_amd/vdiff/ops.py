@@ -468,8 +468,95 @@ class frozen_weights:
         return False
 
 
+class step_packed_weights:
+    """Training-step context (engine.Trainer): the packed conv operands of every Parameter
+    are produced by ONE launch (vd_conv_pack_weights) at the start of each step instead of
+    one pack kernel per conv and direction.  The first step packs per
+    call as usual and records which (weight, layout) operands it needed; at its end the
+    plan is built (persistent operand buffers + a device descriptor table), and every later
+    step's __enter__ re-packs all of them from the current fp32 weights -- after the
+    previous optimizer step, on the current stream -- so the step reads operands of exactly
+    the weights it trains with.  A weight whose storage moved (load_state_dict into a new
+    tensor, .to()) or an operand not in the plan falls back to the per-call pack; the plan
+    is rebuilt at the end of such a step."""
+
+    def __init__(self):
+        self.want = {}     # key -> (param, Co, Ci, taps, Cip, Cop, transpose, dt)
+        self.bufs = {}     # key -> packed operand (valid inside a step after __enter__)
+        self.plans = []    # [(dt, desc table (device uint8), n, total)]
+        self.dirty = False
+        self.active = False
+
+    def __enter__(self):
+        global _step_pack
+        if self.plans:
+            for dt, table, n, total in self.plans:
+                _lib.call("vd_conv_pack_weights", _p(table), n, total, _DT[dt], _stream(table))
+        self.active = True
+        _step_pack = self
+        return self
+
+    def __exit__(self, *exc):
+        global _step_pack
+        _step_pack = None
+        self.active = False
+        if self.dirty and exc[0] is None:
+            self._build()
+        return False
+
+    @staticmethod
+    def key(weight, Cip, Cop, transpose, dt):
+        return (id(weight), weight.data_ptr(), tuple(weight.shape), Cip, Cop, transpose, dt)
+
+    def lookup(self, key):
+        return self.bufs.get(key) if self.plans else None
+
+    def record(self, key, spec):
+        if key not in self.want:
+            self.want[key] = spec
+            self.dirty = True
+
+    def _build(self):
+        import numpy as np
+        live = {k: v for k, v in self.want.items() if v[0].data_ptr() == k[1]}
+        self.want, self.bufs, self.plans, self.dirty = live, {}, [], False
+        by_dt = {}
+        for k, spec in live.items():
+            by_dt.setdefault(spec[7], []).append((k, spec))
+        desc = np.dtype([("w", "<u8"), ("out", "<u8"), ("Co", "<i4"), ("Ci", "<i4"),
+                         ("taps", "<i4"), ("Cip", "<i4"), ("Cop", "<i4"), ("tr", "<i4"),
+                         ("start", "<i8")])
+        for dt, jobs in by_dt.items():
+            for c0 in range(0, len(jobs), 1024):
+                chunk = jobs[c0:c0 + 1024]
+                rows = np.zeros(len(chunk), desc)
+                total = 0
+                for r, (k, (w, Co, Ci, taps, Cip, Cop, tr, _)) in enumerate(chunk):
+                    shape = (Cip, taps, Cop) if tr else (Co, taps, Cip)
+                    out = torch.empty(shape, dtype=dt, device=w.device)
+                    self.bufs[k] = out
+                    if w.dtype != torch.float32 or not w.is_contiguous():
+                        raise ValueError("packed weights: fp32 contiguous parameters only")
+                    rows[r] = (w.data_ptr(), out.data_ptr(), Co, Ci, taps, Cip, Cop, int(tr),
+                               total)
+                    total += out.numel()
+                table = torch.from_numpy(rows.view(np.uint8).copy()).to(chunk[0][1][0].device)
+                self.plans.append((dt, table, len(chunk), total))
+
+
+_step_pack = None
+
+
 def _pack_weight(weight, Co, Ci, taps, Cip, Cop, transpose, dt):
     """torch [Co][Ci][*k] weight -> packed fwd [Co][taps][Cip] / bwd [Cip][taps][Cop] operand."""
+    sp = _step_pack
+    if (sp is not None and isinstance(weight, torch.nn.Parameter)
+            and weight.dtype == torch.float32 and weight.is_contiguous()):
+        k = sp.key(weight, Cip, Cop, transpose, dt)
+        hit = sp.lookup(k)
+        if hit is not None:
+            return hit
+        sp.record(k, (weight, Co, Ci, taps, Cip, Cop, transpose, dt))
     key = None
     # parameters only: a temporary (a padded or stacked weight) may reuse a freed address
     if frozen_weights.depth and isinstance(weight, torch.nn.Parameter):

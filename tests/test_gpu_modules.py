@@ -325,3 +325,49 @@ def test_trainer_step_matches_reference_adam_step():
         assert rel_l2(grads[k], g["grad_" + k]) < 1e-4, k
         d = named[k].detach() - before[k]
         assert adam_delta_close(d, g["delta_" + k], g["grad_" + k]) < 1e-6, k
+
+
+def test_trainer_batched_pack_equals_per_call_pack():
+    """the conv operands re-packed once per step in one launch
+    (ops.step_packed_weights, vd_conv_pack_weights) equal the per-call packs, so three bf16
+    train steps from the same init give bit-identical losses and parameters; from the
+    second step on no per-call pack runs for a Parameter."""
+    import copy
+    from vdiff import ops
+    from vdiff.engine import Clip, Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    from vdiff.unet_audio import UNetAudio
+    m = UNetAudio(image_size=32, in_channels=3, model_channels=32, out_channels=3,
+                  num_res_blocks=1, attention_resolutions=(2,), channel_mult=(1, 2), dims=3,
+                  audio_feature_dim=64, projected_audio_dim=16, im_cond_output_ch=16,
+                  dropout=0.0, audio_encoder=False)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    m.load_state_dict(init_params(shapes, 5))
+    m.convert_to_fp16()
+    m = m.to(dev)
+    runs = []
+    for batch_pack in (False, True):
+        mm = copy.deepcopy(m)
+        tr = Trainer(mm, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-3,
+                     batch_pack=batch_pack)
+        calls = []
+        orig = ops._pack_weight_now
+        ops._pack_weight_now = lambda w, *a, _o=orig: calls.append(w) or _o(w, *a)
+        try:
+            losses = []
+            for s in range(3):
+                gen = torch.Generator(device=dev).manual_seed(s)
+                x0 = torch.rand((1, 3, 4, 32, 32), generator=gen, device=dev) * 2 - 1
+                cond = torch.rand((1, 3, 32, 32), generator=gen, device=dev) * 2 - 1
+                feat = torch.randn((4, 64), generator=gen, device=dev)
+                eps = torch.randn(x0.shape, generator=gen, device=dev)
+                n0 = len(calls)
+                losses.append(tr.step(Clip(x0, cond, feat, eps, torch.tensor([7 + s], device=dev))))
+                if batch_pack and s > 0:
+                    assert not any(isinstance(w, torch.nn.Parameter) for w in calls[n0:])
+        finally:
+            ops._pack_weight_now = orig
+        runs.append((torch.stack(losses), [p.detach().clone() for p in mm.parameters()]))
+    assert torch.equal(runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)

@@ -1,0 +1,78 @@
+"""train.py with the .vdclip data path (--data: memory-mapped clips, GPU frame transform,
+host audio DSP, ClipBatcher's prefetch thread) against the same run on synthetic clips
+generated on the device (the loader must stay off the critical path).
+
+    python tools/data_vs_synth.py [--clips 8] [--epochs 4] [--steps 8]
+
+Writes --clips random clips (256x256 uint8 frames at 30 fps, 44.1 kHz audio, so the
+resample and the antialiased resize both run) under /tmp, builds the FrameItem index, then
+runs the config-2 train step (UNet3D 128x128x16, joint attention, bf16, batch 1 clip) twice
+as child processes (this process never touches the GPU) and prints one JSON line with the
+frames/s of each run's epochs after the first (warm-up) and their ratio."""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "lipreading-video-generation_amd")
+sys.path.insert(0, PKG)
+TRAIN = os.path.join(PKG, "video-generation", "diffusion", "train.py")
+
+
+def make_dataset(d, clips, frames=96, size=256, sr=44100, fps=30.0):
+    from vdiff.data import build_frame_items, save_frame_items, write_clip
+    rng = np.random.default_rng(0)
+    paths = []
+    for i in range(clips):
+        p = os.path.join(d, f"clip{i:03d}.vdclip")
+        fr = rng.integers(0, 256, (frames, size, size, 3), dtype=np.uint8)
+        au = rng.standard_normal((1, int(sr * frames / fps)), dtype=np.float32) * 0.1
+        write_clip(p, fr, fps, au, sr)
+        paths.append(p)
+    index = os.path.join(d, "items.jsonl")
+    save_frame_items(build_frame_items(paths), index)
+    return index
+
+
+def run(extra, epochs, steps, d):
+    cmd = [sys.executable, "-u", TRAIN, "--dims", "3", "--frames", "16", "--image-size", "128",
+           "--batch-size", "1", "--attention-mode", "joint", "--dtype", "bf16",
+           "--random-audio-encoder", "--reinit-nonzero", "--epochs", str(epochs),
+           "--steps-per-epoch", str(steps), "--ckpt", os.path.join(d, "ck.pth")] + extra
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    if out.returncode != 0:
+        sys.stderr.write(out.stdout[-3000:] + out.stderr[-3000:])
+        raise SystemExit(out.returncode)
+    fps = [float(m) for m in re.findall(r"\| ([0-9.]+) frames/s", out.stdout)]
+    return fps, time.time() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clips", type=int, default=8)
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=8)
+    a = ap.parse_args()
+    d = tempfile.mkdtemp(prefix="vdata_", dir="/tmp")
+    index = make_dataset(d, a.clips)
+    synth, ts = run([], a.epochs, a.steps, d)
+    data, td = run(["--data", index], a.epochs, a.steps, d)
+    s, r = float(np.mean(synth[1:])), float(np.mean(data[1:]))
+    print(json.dumps({"synthetic_frames_per_s": round(s, 3), "data_frames_per_s": round(r, 3),
+                      "data_over_synthetic": round(r / s, 4), "epochs_synthetic": synth,
+                      "epochs_data": data, "steps_per_epoch": a.steps, "clips": a.clips,
+                      "wall_s": [round(ts, 1), round(td, 1)],
+                      "workload": "train.py config 2: UNet3D 128x128x16 joint bf16, 1 clip, "
+                                  "256x256 uint8 frames + 44.1 kHz audio (.vdclip)"}))
+
+
+if __name__ == "__main__":
+    main()
