@@ -481,17 +481,19 @@ def gen_dq(probe=None):
 def main():
     out = sys.argv[1]
     from gen_d128 import gen_dkdv128, gen_dq128
+    from gen_fwd128 import gen_fwd128
     from gen_fwd import gen_fwd
     kdq, ddq, sdq = gen_dq()
     kdk, ddk, sdk = gen_dkdv()
     kfw, sfw = gen_fwd()
     kdk2, ddk2, sdk2 = gen_dkdv128()
     kdq2, sdq2 = gen_dq128()
+    kfw2, dfw2, sfw2 = gen_fwd128()
     with open(out, "w") as f:
         f.write("// generated by gen_attn_asm.py -- do not edit\n")
-        f.write(code_object_text([kdq, kdk, kfw, kdk2, kdq2], ddq + ddk + ddk2))
+        f.write(code_object_text([kdq, kdk, kfw, kdk2, kdq2, kfw2], ddq + ddk + ddk2 + dfw2))
     if "--report" in sys.argv:
-        for name, st in (("dq", sdq), ("dkdv", sdk), ("fwd", sfw), ("dkdv128", sdk2), ("dq128", sdq2)):
+        for name, st in (("dq", sdq), ("dkdv", sdk), ("fwd", sfw), ("dkdv128", sdk2), ("dq128", sdq2), ("fwd128", sfw2)):
             print(f"{name}: {len(st.lines)} lines, {st.nops} nop wait states, {st.waits} lgkm "
                   f"waits, {st.forced} forced by the 15-read limit ({st.young} on young reads)")
 

@@ -1844,7 +1844,8 @@ int check_attn(const vd_attn_desc* d) {
 //          each LDS fragment feeds two MFMAs; bf16, D = 64; fwd keeps its default)
 //   kSP: retired (the fragment-pipelined backward measured equal to kP8, which it now
 //          selects; profiles/r02_ab_sp.txt)
-//   kAsm: the hand-scheduled head_dim-64 backward (asm/gen_attn_asm.py), one wave per SIMD
+//   kAsm: the hand-scheduled kernels (asm/): head_dim-64 forward and backward, head_dim-128
+//          backward; one wave per SIMD
 //   kP8 / kP4 forward: retired (5 % slower than the deferred-check forward, which they select)
 enum AttnCfg { kBase = 0, kNB2 = 1, kW8 = 2, kP8 = 3, kP4 = 4, kD8 = 5, kD8N = 6, kD4 = 7,
                kPair = 8, kP4N2 = 9, kRole = 10, kSP = 11, kAsm = 12, kCfgLast = kAsm };
@@ -1881,17 +1882,18 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //            (round 2) 3.84-3.96 vs base 4.84-4.85 ms on the same box (tools/ab_d128.sh)
   //   D = 64 backward (round 3): hand-scheduled dQ 18.8 / dK/dV 24.6 ms vs P8 20.8 / 28.9 ms
   //            on the same box (tools/gpu_asm.sh)
+  //   D = 128 backward (round 3): hand-scheduled dQ 2.55-2.60 / dK/dV 3.37-3.40 ms vs W8 2.96 /
+  //            PAIR 3.97-3.99 ms on the same box (tools/gpu_asm128.sh)
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
       !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
-      !(env == kAsm && D != 64 && !(D == 128 && kind != 0)) &&  // hand-scheduled: D = 64,
-                                                     // D = 128 backward
+      !(env == kAsm && D != 64 && D != 128) &&       // hand-scheduled: D = 64, 128
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kAsm;  // falls back to D8N / P8 off its shapes
-  else if (D == 128) c = kind == 0 ? kD8N : (kind == 1 ? kW8 : kPair);
+  else if (D == 128) c = kind == 0 ? kD8N : kAsm;  // asm falls back to W8 / PAIR off its shapes
   else if (D == 256 && kind == 2) c = kRole;
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
@@ -2043,15 +2045,18 @@ inline bool asm_dq_ok(const vd_attn_desc* d, const void* q, const void* k, const
 // (the DMA runs up to 12 tiles past the end of the sequence: the 512-key rounding plus the
 // 4-tile prefetch) and a 4-byte aligned lse
 inline bool asm_fwd_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
-                       const void* o, const float* lse) {
+                       const void* o, const float* lse, int D = 64) {
   const int64_t n = d->seq_len;
-  return asm_dq_ok(d, q, k, v, o, o) && (n + 1024) * d->token_stride * 2 < 0x7fffffffLL &&
+  return asm_dq_ok(d, q, k, v, o, o, D) && (n + 1024) * d->token_stride * 2 < 0x7fffffffLL &&
          ((uintptr_t)lse & 3) == 0;
 }
 
+// hand-scheduled forward: head_dim 64 (64-key tiles, asm/gen_fwd.py) or 128 (32-key tiles,
+// asm/gen_fwd128.py); 8 tiles per iteration, the last iteration masked
 int fwd_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
                    float* lse, hipStream_t st) {
   const int64_t n = d->seq_len;
+  const int D = d->head_dim, TR = D == 128 ? 32 : 64;
   vd::AsmFwdArgs a{};
   a.q = q; a.k = k; a.v = v; a.o = o; a.lse = lse;
   a.n = (uint32_t)n;
@@ -2063,13 +2068,14 @@ int fwd_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
   a.obs_bytes = (uint64_t)d->o_batch_stride * 2;
   a.ogs_bytes = (uint64_t)d->o_group_stride * 2;
   a.qscale = d->scale * kLog2e;  // the fp32 product RowFrag::scale receives
-  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 64) * 2);
-  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 64) * 2);
-  a.tile_bytes = (uint32_t)(kTile * d->token_stride * 2);
-  a.niter = (uint32_t)vd_cdiv(n, 512);
-  a.klim0 = (uint32_t)(n - 512 * (int64_t)(a.niter - 1));
-  const int rc = vd::asm_fwd_d64(a, (unsigned)vd_cdiv(n, 256), (unsigned)d->groups,
-                                 (unsigned)(d->nseq / d->groups), st);
+  a.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + D) * 2);
+  a.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + D) * 2);
+  a.tile_bytes = (uint32_t)(TR * d->token_stride * 2);
+  a.niter = (uint32_t)vd_cdiv(n, 8 * TR);
+  a.klim0 = (uint32_t)(n - 8 * TR * (int64_t)(a.niter - 1));
+  const unsigned gx = (unsigned)vd_cdiv(n, 256), gy = (unsigned)d->groups,
+                 gz = (unsigned)(d->nseq / d->groups);
+  const int rc = D == 128 ? vd::asm_fwd_d128(a, gx, gy, gz, st) : vd::asm_fwd_d64(a, gx, gy, gz, st);
   return rc ? rc : vd::check_launch("attn_fwd");
 }
 
@@ -2092,7 +2098,10 @@ int fwd_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const 
       if (c == kD4) return fwd_defer_launch<T, D, 4, false>(d, q, k, v, o, lse, st);
     }
     if constexpr (D == 128)
-      if (c == kD8N) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
+      if (c == kAsm && asm_fwd_ok(d, q, k, v, o, lse, D))
+        return fwd_asm_launch(d, q, k, v, o, lse, st);
+    if constexpr (D == 128)
+      if (c == kD8N || c == kAsm) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
     if constexpr (D == 64 || D == 128)  // the pipelined forward is retired: its successor
       if (c == kP4) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
   }

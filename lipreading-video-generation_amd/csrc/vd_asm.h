@@ -77,4 +77,8 @@ static_assert(sizeof(AsmFwdArgs) == 112, "kernarg block layout");
 // grid (ceil(n / 256), groups, nseq / groups), 256 threads, 128 KiB static LDS
 int asm_fwd_d64(const AsmFwdArgs& a, unsigned gx, unsigned gy, unsigned gz, hipStream_t stream);
 
+// vd_attn_fwd_d128 (asm/gen_fwd128.py): the same block with 32-row tiles (tile_bytes, niter
+// = 256-key iterations, klim0); grid (ceil(n / 256), groups, nseq / groups), 128 KiB LDS
+int asm_fwd_d128(const AsmFwdArgs& a, unsigned gx, unsigned gy, unsigned gz, hipStream_t stream);
+
 }  // namespace vd

@@ -88,3 +88,76 @@ def test_asm128_against_fp32_reference():
     for got, ref in ((gr[0, :C], q.grad), (gr[0, C:2 * C], k.grad), (gr[0, 2 * C:], v.grad)):
         e = float((got.float().T - ref).norm() / ref.norm())
         assert e < 2e-2, e
+
+
+# ------------------------------------------------------------------ forward (gen_fwd128.py)
+def _fwd(qkv, cfg, **kw):
+    from vdiff import ops
+    x = qkv.detach().clone().requires_grad_(True)
+    with ops.attention_config(cfg):
+        y = ops.attention(x, 1, **kw)
+    lse = y.grad_fn.saved_tensors[2].detach().clone()
+    torch.cuda.synchronize()
+    return y.detach(), lse
+
+
+def _reference(qkv):
+    t = qkv.float()[0].detach()
+    q, k, v = t[:C].T, t[C:2 * C].T, t[2 * C:].T
+    s = (q @ k.T) / math.sqrt(C)
+    return torch.softmax(s, -1) @ v, torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("B,N,seed", [(1, 1024, 20), (1, 1500, 21), (1, 4096, 22),
+                                      (2, 3000, 23), (1, 65536 + 17, 24)])
+def test_asm128_fwd_against_deferred_check_kernel(B, N, seed):
+    """vd_attn_fwd_d128 runs the deferred-check forward's algorithm (lagged max, bf16 P,
+    fp32 row sums) with 32-key tiles and another summation order: O to bf16 rounding, lse
+    to 2e-5."""
+    qkv, _ = _inputs(B, N, seed)
+    y0, l0 = _fwd(qkv, "d8n")
+    y1, l1 = _fwd(qkv, "asm")
+    assert torch.isfinite(y1.float()).all() and torch.isfinite(l1).all()
+    assert _rel(y1, y0) <= 4e-3
+    assert float((l1 - l0).abs().max()) <= 2e-5
+
+
+def test_asm128_fwd_against_fp32_reference():
+    qkv, _ = _inputs(1, 4096, 25)
+    y, lse = _fwd(qkv, "asm")
+    yd, ld = _fwd(qkv, "d8n")
+    ref, lref = _reference(qkv)
+    e, ed = _rel(y[0].T, ref), _rel(yd[0].T, ref)
+    assert e <= max(1.25 * ed, 4e-3), (e, ed)
+    el, eld = float((lse - lref).abs().max()), float((ld - lref).abs().max())
+    assert el <= 1.25 * eld + 1e-5, (el, eld)
+
+
+def test_asm128_fwd_late_logit_jumps():
+    """Keys far above every earlier score in late tiles (the rare path past the first tile,
+    in an unmasked iteration and in the masked last one) and a query with a large max."""
+    from vdiff import ops
+    N = 3000
+    gen = torch.Generator(device=dev).manual_seed(26)
+    qkv = torch.randn((1, 3 * C, N), generator=gen, device=dev) * 2.0
+    qkv[:, C:2 * C, 700] *= 12
+    qkv[:, C:2 * C, 2900] *= 14
+    qkv[:, :C, 1300] *= 10
+    qkv = ops.to_cl(qkv.bfloat16())
+    y, lse = _fwd(qkv, "asm")
+    yd, ld = _fwd(qkv, "d8n")
+    ref, lref = _reference(qkv)
+    assert torch.isfinite(y.float()).all()
+    assert _rel(y[0].T, ref) < 2e-2
+    assert _rel(y, yd) <= 1e-2
+    el, eld = float((lse - lref).abs().max()), float((ld - lref).abs().max())
+    assert el <= 1.25 * eld + 1e-5, (el, eld)
+
+
+def test_asm128_fwd_spatial_groups():
+    qkv, _ = _inputs(1, None, 27, spatial=(4, 32, 32))
+    kw = dict(mode="spatial", spatial=(4, 32, 32))
+    y0, l0 = _fwd(qkv, "d8n", **kw)
+    y1, l1 = _fwd(qkv, "asm", **kw)
+    assert _rel(y1, y0) <= 4e-3
+    assert float((l1 - l0).abs().max()) <= 2e-5

@@ -329,9 +329,10 @@ def test_trainer_step_matches_reference_adam_step():
 
 def test_trainer_batched_pack_equals_per_call_pack():
     """the conv operands re-packed once per step in one launch
-    (ops.step_packed_weights, vd_conv_pack_weights) equal the per-call packs, so three bf16
-    train steps from the same init give bit-identical losses and parameters; from the
-    second step on no per-call pack runs for a Parameter."""
+    (ops.step_packed_weights, vd_conv_pack_weights) are bit-identical to per-call packs of
+    the same weights, from the second step on no per-call pack runs for a Parameter, and
+    three bf16 train steps track the per-call run (the split-K weight-gradient atomics make
+    runs differ in the last fp32 bits, so parameters are compared at 1e-5)."""
     import copy
     from vdiff import ops
     from vdiff.engine import Clip, Trainer
@@ -368,6 +369,12 @@ def test_trainer_batched_pack_equals_per_call_pack():
         finally:
             ops._pack_weight_now = orig
         runs.append((torch.stack(losses), [p.detach().clone() for p in mm.parameters()]))
-    assert torch.equal(runs[0][0], runs[1][0])
+    # the batched launch against per-call packs of the current weights: bit-identical
+    sp = tr.packs
+    assert len(sp.bufs) >= 20
+    with sp:
+        for k, (w, Co, Ci, taps, Cip, Cop, trn, dt) in sp.want.items():
+            assert torch.equal(sp.bufs[k], ops._pack_weight_now(w, Co, Ci, taps, Cip, Cop, trn, dt))
+    assert rel_l2(runs[1][0], runs[0][0]) < 1e-5
     for a, b in zip(runs[0][1], runs[1][1]):
-        assert torch.equal(a, b)
+        assert rel_l2(b, a) < 1e-5
