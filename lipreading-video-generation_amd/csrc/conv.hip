@@ -19,6 +19,7 @@
 // registers -> LDS (double buffered, one barrier per K step); LDS rows of
 // 64 B use a chunk XOR swizzle that is conflict-free for the fragment reads.
 #include "vd_common.h"
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <atomic>
@@ -1924,7 +1925,17 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     // LDS-DMA kernels: kw-strip (three taps per workgroup) or 1x1 (a plain GEMM over pixels)
     const int wc = one ? 64 : (d->Wo < 64 ? d->Wo : 64);
     const int rows = one ? 64 : (64 / wc) * (wc + 2);
-    const int cot = 64;
+    // 1x1 (A/B knob VDIFF_WGRAD1=nst,cot): ring depth 2 / 4 / 6 and 64 / 128 / 192 output
+    // channels per workgroup (192: X read once per 192 channels of the qkv projections)
+    static const int w1 = [] {
+      const char* e = getenv("VDIFF_WGRAD1");
+      int n = 2, c = 64;
+      if (e) sscanf(e, "%d,%d", &n, &c);
+      return n * 1000 + c;
+    }();
+    const int w1_nst = w1 / 1000, w1_cot = (w1 % 1000 == 192 && d->Co % 192 == 0) ? 192
+                                             : (w1 % 1000 == 128 && d->Co % 128 == 0 ? 128 : 64);
+    const int cot = one ? w1_cot : 64;
     // nine-tap planes (VDIFF_CONV_WPLANE=1, A/B): image rows of whole 64-pixel steps
     static const int wplane = [] {
       const char* e = getenv("VDIFF_CONV_WPLANE");
@@ -1954,7 +1965,13 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
   } while (0)
     // 64 x 64 tiles, double-buffered (40 KiB at RW = 96: three workgroups per CU).
     // Measured against COT = 128 and a three-stage ring: both slower (tools/conv_ab.sh).
-    if (one) VD_WGD(64, 64, 2, true);
+    if (one && cot == 192 && w1_nst >= 4) VD_WGD(64, 192, 4, true);
+    else if (one && cot == 192) VD_WGD(64, 192, 2, true);
+    else if (one && cot == 128 && w1_nst >= 4) VD_WGD(64, 128, 4, true);
+    else if (one && cot == 128) VD_WGD(64, 128, 2, true);
+    else if (one && w1_nst >= 6) VD_WGD(64, 64, 6, true);
+    else if (one && w1_nst >= 4) VD_WGD(64, 64, 4, true);
+    else if (one) VD_WGD(64, 64, 2, true);
     else if (plane) VD_WGD(224, 64, 2, false, true);
     else if (rows <= 96) VD_WGD(96, 64, 2, false);
     else if (rows <= 128) VD_WGD(128, 64, 2, false);
