@@ -41,7 +41,8 @@ NINF, PINF = "0xff800000", "0x7f800000"
 BAR2 = False           # A/B (tools/asm_ab.py): one barrier per two bodies
 CHECK_NOP = 3          # wait states between the check's v_cmp and its branch
 DROP = 0               # timing experiments only (wrong results): 1 exp, 2 add, 4 cvt, 8 reads
-CHAINS = 4             # row-sum accumulators per query block (1: one dependent add chain)
+CHAINS = 1             # row-sum accumulators per query block (1: one dependent add chain;
+                       # 14.24 vs 14.42 ms for 4, profiles/r03_ab_fwd_knobs.txt)
 NORARE = 0             # timing experiment only: never take the rare path (wrong results)
 STAMP = 0              # diagnostic: store loop cycles / realtime per workgroup (karg 112)
 GSGS = 0               # MFMA order of a body: 0 G(kb0) G(kb1) S(kb0) S(kb1); 1 G S G S

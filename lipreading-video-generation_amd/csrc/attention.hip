@@ -1883,7 +1883,8 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //   D = 64 backward (round 3): hand-scheduled dQ 18.8 / dK/dV 24.6 ms vs P8 20.8 / 28.9 ms
   //            on the same box (tools/gpu_asm.sh)
   //   D = 128 backward (round 3): hand-scheduled dQ 2.55-2.60 / dK/dV 3.37-3.40 ms vs W8 2.96 /
-  //            PAIR 3.97-3.99 ms on the same box (tools/gpu_asm128.sh)
+  //            PAIR 3.97-3.99 ms on the same box (tools/gpu_asm128.sh); forward 1.67-1.68 vs
+  //            D8N 2.04-2.05 ms (tools/gpu_r03c.sh)
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
@@ -1893,7 +1894,7 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kAsm;  // falls back to D8N / P8 off its shapes
-  else if (D == 128) c = kind == 0 ? kD8N : kAsm;  // asm falls back to W8 / PAIR off its shapes
+  else if (D == 128) c = kAsm;  // asm falls back to D8N / W8 / PAIR off its shapes
   else if (D == 256 && kind == 2) c = kRole;
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each

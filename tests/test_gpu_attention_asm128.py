@@ -161,3 +161,11 @@ def test_asm128_fwd_spatial_groups():
     y1, l1 = _fwd(qkv, "asm", **kw)
     assert _rel(y1, y0) <= 4e-3
     assert float((l1 - l0).abs().max()) <= 2e-5
+
+
+def test_asm128_is_the_d128_default():
+    qkv, g = _inputs(1, 2048, 28)
+    y0, l0 = _fwd(qkv, "auto")
+    y1, l1 = _fwd(qkv, "asm")
+    assert torch.equal(y0, y1) and torch.equal(l0, l1)
+    assert torch.equal(_grads(qkv, g, "auto", "auto"), _grads(qkv, g, "asm", "asm"))
