@@ -46,6 +46,8 @@ CHAINS = 1             # row-sum accumulators per query block (1: one dependent 
 NORARE = 0             # timing experiment only: never take the rare path (wrong results)
 STAMP = 0              # diagnostic: store loop cycles / realtime per workgroup (karg 112)
 GSGS = 0               # MFMA order of a body: 0 G(kb0) G(kb1) S(kb0) S(kb1); 1 G S G S
+MSUM = 0               # row sums on the matrix pipe: 8 MFMAs (ones x P^T) per body replace the
+                       # 64 v_add_f32; the tile's lagged-max check moves to the next body's top
 
 # kernel arguments (AsmFwdArgs in vd_asm.h), loaded into s[16:43]:
 #  0 q  8 k  16 v  24 o  32 lse                            (u64)   s16..s25
@@ -74,6 +76,9 @@ def regs():
     A.alloc("acc", 64)       # O^T accumulators [i][j]
     A.alloc("kf", 32)        # K row fragments [kb][s]
     A.alloc("trf", 32)       # V^T fragments [kb][i][s2] (lo 2 + hi 2)
+    if MSUM:
+        A.alloc("lsum", 32)  # tile row sums [j] (all 16 rows of a block hold the lane's sum)
+        A.alloc("ones", 4)   # bf16 1.0 A operand
     return V, A
 
 
@@ -120,6 +125,19 @@ def g_mfmas(V, A, kb):
     return out
 
 
+def sum_mfmas(V, A):
+    """MSUM: lsum[j] = sum over the tile's 64 keys of P^T (bf16, the PV operand) for the
+    lane's query -- ones[32 x 16] x P^T[kb][j][s2], both lane halves get the full sum."""
+    out = []
+    for j in range(2):
+        acc = A.r("lsum", 16 * j, 16)
+        for n, (kb, s2) in enumerate((kb, s2) for kb in range(2) for s2 in range(2)):
+            c = "0" if n == 0 else acc
+            out.append((f"{MFMA} {acc}, {A.r('ones', 0, 4)}, "
+                        f"{V.r('p', 8 * (2 * kb + j) + 4 * s2, 4)}, {c}", ()))
+    return out
+
+
 def s_mfmas(V, A, par, kb, zero_c=False):
     """S'(kb) of both query blocks into accumulator set `par` (srcC: -m, or 0)."""
     out = []
@@ -146,6 +164,20 @@ def softmax_list(V, par, masked, u):
     kinds = {"v_exp_f32": 1, "v_add_f32": 2, "v_mov_b32": 2, "v_cvt_pk_bf16_f32": 4}
     gk = {0: 9, 1: 25} if GSGS else {0: 9, 1: 17}
     out = []
+    if MSUM:
+        for kb in range(2):
+            for j in range(2):
+                p = 2 * kb + j
+                S = V[f"s{par}"] + 16 * p
+                out += mask_list(V, S, masked, u, kb)
+                for k in range(0, 8, 2):  # 4 exps, then their 2 packs (no trans hazard)
+                    for x in range(4):
+                        out.append((f"v_exp_f32 v{S + 2 * k + x}, v{S + 2 * k + x}",
+                                    COST["exp"], 0))
+                    for kk in (k, k + 1):
+                        out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + kk)}, v{S + 2 * kk}, "
+                                    f"v{S + 2 * kk + 1}", COST["cvt"], gk[kb]))
+        return [it for it in out if not DROP & kinds.get(it[0].split()[0], 0)]
     if CHAINS == 1:
         for kb in range(2):
             for j in range(2):
@@ -363,6 +395,12 @@ def prologue(st: Stream, V, A):
         e(f"v_mov_b32 {V.r('l', j)}, 0")
         e(f"v_mov_b32 {V.r('ps', j)}, 0")
     e(f"v_mov_b32 {V.r('ninf')}, {NINF}")
+    if MSUM:  # the "tile -1" check of the first body passes (sum 0)
+        e(f"v_mov_b32 {V.r('tmp', 0)}, 0x3f803f80")
+        for k in range(4):
+            e(f"v_accvgpr_write_b32 {A.r('ones', k)}, {V.r('tmp', 0)}")
+        for k in range(32):
+            e(f"v_accvgpr_write_b32 {A.r('lsum', k)}, 0")
     for t in range(PD):
         dma_tile(st, V, t)
 
@@ -389,11 +427,40 @@ def dma_tile(st: Stream, V, stage):
 
 
 # ------------------------------------------------------------------ one body
-def emit_body(st: Stream, V, A, u, masked, tag):
+def emit_check(st: Stream, V, A, u, masked, tag, msum):
+    """Lagged-max check of the tile in stage u: any lane's tile sum >= 2^16 (or inf / NaN)
+    -> the rare path; then l += the tile sum.  msum: the sum is read from the lsum MFMA
+    accumulators (both lane halves hold the full sum)."""
+    par = u % 2
+    kst = (u + 1) % NST
+    tc = V.r("tc", 0)
+    if msum:
+        for j in range(2):
+            st.emit(f"v_accvgpr_read_b32 {V.r('ps', j)}, {A.r('lsum', 16 * j)}")
+    st.emit(f"v_max_f32 {tc}, {V.r('ps', 0)}, {V.r('ps', 1)}")
+    st.emit(f"v_cmp_ngt_f32 vcc, 0x47800000, {tc}")
+    if CHECK_NOP:
+        st.raw(f"s_nop {CHECK_NOP}")
+    st.raw(f"s_cbranch_vccz .Lfwd_ok{tag}")
+    if NORARE:
+        st.raw(f"s_branch .Lfwd_ok{tag}")
+    st.raw(f"s_mov_b32 {S_ST}, {u * STAGE}")
+    st.raw(f"s_mov_b32 {S_ST1}, {kst * STAGE}")
+    st.raw(f"s_mov_b32 {S_KB}, {64 * u}")
+    v = 2 * int(masked) + par
+    st.raw(f"s_swappc_b64 {S_RET}, s[{S_TGT + 2 * v}:{S_TGT + 2 * v + 1}]")
+    st.label(f".Lfwd_ok{tag}")
+    for j in range(2):
+        st.emit(f"v_add_f32 {V.r('l', j)}, {V.r('l', j)}, {V.r('ps', j)}")
+
+
+def emit_body(st: Stream, V, A, u, masked, tag, prev=None):
     """Body of tile t (ring stage u = t mod 8): G(t-1), S(t+1), the softmax of tile t, the
-    lagged-max check of tile t."""
+    lagged-max check of tile t (MSUM: of tile t-1 at the top, prev = its (u, masked))."""
     par = u % 2
     st.comment(f"---- body, stage {u}{' (masked)' if masked else ''}")
+    if MSUM:
+        return emit_body_msum(st, V, A, u, masked, tag, prev)
     if not BAR2:
         st.raw(f"s_waitcnt vmcnt({(PD - 2) * 4}) lgkmcnt(0)")  # tile t+1 landed
         st.raw("s_barrier")
@@ -443,22 +510,55 @@ def emit_body(st: Stream, V, A, u, masked, tag):
         text, deps = mf[g]
         st.emit(text, wait_lds=deps)
     # lagged-max check of tile t: any lane's tile sum >= 2^16 (or inf / NaN) -> rare path
-    tc = V.r("tc", 0)
-    st.emit(f"v_max_f32 {tc}, {V.r('ps', 0)}, {V.r('ps', 1)}")
-    st.emit(f"v_cmp_ngt_f32 vcc, 0x47800000, {tc}")
-    if CHECK_NOP:
-        st.raw(f"s_nop {CHECK_NOP}")
-    st.raw(f"s_cbranch_vccz .Lfwd_ok{tag}")
-    if NORARE:
-        st.raw(f"s_branch .Lfwd_ok{tag}")
-    st.raw(f"s_mov_b32 {S_ST}, {u * STAGE}")
-    st.raw(f"s_mov_b32 {S_ST1}, {kst * STAGE}")
-    st.raw(f"s_mov_b32 {S_KB}, {64 * u}")
-    v = 2 * int(masked) + par
-    st.raw(f"s_swappc_b64 {S_RET}, s[{S_TGT + 2 * v}:{S_TGT + 2 * v + 1}]")
-    st.label(f".Lfwd_ok{tag}")
-    for j in range(2):
-        st.emit(f"v_add_f32 {V.r('l', j)}, {V.r('l', j)}, {V.r('ps', j)}")
+    emit_check(st, V, A, u, masked, tag, False)
+
+
+def emit_body_msum(st: Stream, V, A, u, masked, tag, prev):
+    """MSUM body t: the check of tile t-1 (prev) after the barrier, then
+    G(t-1) kb0 | G(t-1) kb1 | S(t+1) kb0 | SUM(t) | S(t+1) kb1 (40 MFMAs) with tile t's
+    softmax (exp + cvt only) in gaps 0..23, so P^T(t) is complete before SUM(t)."""
+    par = u % 2
+    st.raw(f"s_waitcnt vmcnt({(PD - 2) * 4}) lgkmcnt(0)")  # tile t+1 landed
+    st.raw("s_barrier")
+    st.flush_lds()
+    if prev is not None:
+        if u == 0 and not masked:
+            st.raw("s_nop 7")  # the loop back edge: SUM(t-1) of the last body wrote lsum
+        emit_check(st, V, A, prev[0], prev[1], f"c{tag}", True)
+    mf = (g_mfmas(V, A, 0) + g_mfmas(V, A, 1) + s_mfmas(V, A, 1 - par, 0) + sum_mfmas(V, A)
+          + s_mfmas(V, A, 1 - par, 1))
+    nm = len(mf)
+    reads = {}
+
+    def put(slot0, lst, per=2):
+        for k, item in enumerate(lst):
+            reads.setdefault(slot0 + k // per, []).append(item)
+
+    kst = (u + 1) % NST
+    if not DROP & 8:
+        put(2, k_reads(V, A, kst, 0))   # K(t+1) rows kb0 (S kb0 at 16..23)
+        put(12, k_reads(V, A, kst, 1))  # kb1 (S kb1 at 32..39)
+        put(24, tr_reads(V, A, u, 0))   # V(t)^T for G(t) in the next body
+        put(32, tr_reads(V, A, u, 1))
+    ops, adv = dma_ops(V, (u + PD) % NST)
+    dma_at = {4: 0, 12: 1, 34: 2, 38: 3}
+    valu = place(softmax_list(V, par, masked, u), 24)
+    for g in range(nm):
+        if g in dma_at:
+            m0, ld = ops[dma_at[g]]
+            st.raw(m0)
+            st.raw("s_nop 0")
+            st.emit(ld)
+            if dma_at[g] == 3:
+                for a in adv:
+                    st.emit(a)
+        for text, rid in reads.get(g, []):
+            st.emit(text, lds_id=rid)
+        if g < 24:
+            for text in valu[g]:
+                st.emit(text)
+        text, deps = mf[g]
+        st.emit(text, wait_lds=deps)
 
 
 def emit_tail(st: Stream, V, A):
@@ -476,11 +576,13 @@ def epilogue(st: Stream, V, A):
     ad, lx, inv = V["s0"] + 8, V["s0"] + 10, V["s0"] + 12
     e(f"v_xor_b32 v{ad}, 32, {V.r('lane')}")
     e(f"v_lshlrev_b32 v{ad}, 2, v{ad}")
+    if not MSUM:  # each lane half summed its own 32 keys of every tile
+        for j in range(2):
+            e(f"ds_bpermute_b32 v{lx + j}, v{ad}, {V.r('l', j)}")
+        st.raw("s_waitcnt lgkmcnt(0)")
+        for j in range(2):
+            e(f"v_add_f32 {V.r('l', j)}, {V.r('l', j)}, v{lx + j}")
     for j in range(2):
-        e(f"ds_bpermute_b32 v{lx + j}, v{ad}, {V.r('l', j)}")
-    st.raw("s_waitcnt lgkmcnt(0)")
-    for j in range(2):
-        e(f"v_add_f32 {V.r('l', j)}, {V.r('l', j)}, v{lx + j}")
         e(f"v_rcp_f32 v{inv + j}, {V.r('l', j)}")
     for j in range(2):
         for i in range(2):
@@ -603,6 +705,16 @@ def rare_path(V, A, par, masked):
                     e(f"v_add_f32 {ps}, {ps}, v{a}")
                     e(f"v_add_f32 {ps}, {ps}, v{b}")
                 e(f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + k)}, v{a}, v{b}")
+    if MSUM:  # the check's sums are per lane over both halves: add the partner half's
+        t0, t1 = V.r("tmp", 0), V.r("tmp", 1)
+        e(f"v_xor_b32 {t0}, 32, {V.r('lane')}")
+        e(f"v_lshlrev_b32 {t0}, 2, {t0}")
+        for j in range(2):
+            e(f"ds_bpermute_b32 {V.r('tmp', 2 + j)}, {t0}, {V.r('ps', j)}")
+        r("s_waitcnt lgkmcnt(0)")
+        for j in range(2):
+            e(f"v_add_f32 {V.r('ps', j)}, {V.r('ps', j)}, {V.r('tmp', 2 + j)}")
+        del t1
     # S(t+1) against m_new
     ta = [V.r("tmp", k) for k in range(4)]
     reads_from(S_ST1)
@@ -653,12 +765,15 @@ def gen_fwd(probe=None):
         st.raw("s_memrealtime s[92:93]")
     st.label(".Lfwd_loop")
     for u in range(NST):
-        emit_body(st, V, A, u, False, f"{u}")
+        emit_body(st, V, A, u, False, f"{u}", prev=((u - 1) % NST, False))
     st.raw(f"s_sub_u32 {S_ITER}, {S_ITER}, 1")
     st.raw(f"s_cmp_lg_u32 {S_ITER}, 0")
     st.raw("s_cbranch_scc1 .Lfwd_loop")
     for u in range(NST):
-        emit_body(st, V, A, u, True, f"m{u}")
+        emit_body(st, V, A, u, True, f"m{u}", prev=((u - 1) % NST, u > 0))
+    if MSUM:  # the last tile's check
+        st.raw("s_waitcnt lgkmcnt(0)")
+        emit_check(st, V, A, NST - 1, True, "last", True)
     emit_tail(st, V, A)
     if STAMP:
         emit_stamp(st, V)
