@@ -1926,10 +1926,12 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     const int wc = one ? 64 : (d->Wo < 64 ? d->Wo : 64);
     const int rows = one ? 64 : (64 / wc) * (wc + 2);
     // 1x1 (A/B knob VDIFF_WGRAD1=nst,cot): ring depth 2 / 4 / 6 and 64 / 128 / 192 output
-    // channels per workgroup (192: X read once per 192 channels of the qkv projections)
+    // channels per workgroup (192: X read once per 192 channels of the qkv projections).
+    // Default 4,128: the train step's 1x1 weight gradients 0.864 -> 0.722 ms on one box
+    // (tools/wgrad1x1_bench.py, profiles/r03_ab_wgrad1x1.txt)
     static const int w1 = [] {
       const char* e = getenv("VDIFF_WGRAD1");
-      int n = 2, c = 64;
+      int n = 4, c = 128;
       if (e) sscanf(e, "%d,%d", &n, &c);
       return n * 1000 + c;
     }();

@@ -58,7 +58,7 @@ def run(extra, epochs, steps, d):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clips", type=int, default=8)
-    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--epochs", type=int, default=7)
     ap.add_argument("--steps", type=int, default=8)
     a = ap.parse_args()
     d = tempfile.mkdtemp(prefix="vdata_", dir="/tmp")
@@ -66,8 +66,11 @@ def main():
     synth, ts = run([], a.epochs, a.steps, d)
     data, td = run(["--data", index], a.epochs, a.steps, d)
     s, r = float(np.mean(synth[1:])), float(np.mean(data[1:]))
+    sm, rm = float(np.median(synth[1:])), float(np.median(data[1:]))
     print(json.dumps({"synthetic_frames_per_s": round(s, 3), "data_frames_per_s": round(r, 3),
-                      "data_over_synthetic": round(r / s, 4), "epochs_synthetic": synth,
+                      "data_over_synthetic": round(r / s, 4),
+                      "median_synthetic": round(sm, 3), "median_data": round(rm, 3),
+                      "median_ratio": round(rm / sm, 4), "epochs_synthetic": synth,
                       "epochs_data": data, "steps_per_epoch": a.steps, "clips": a.clips,
                       "wall_s": [round(ts, 1), round(td, 1)],
                       "workload": "train.py config 2: UNet3D 128x128x16 joint bf16, 1 clip, "
