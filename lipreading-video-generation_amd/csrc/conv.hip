@@ -1937,7 +1937,16 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     }();
     const int w1_nst = w1 / 1000, w1_cot = (w1 % 1000 == 192 && d->Co % 192 == 0) ? 192
                                              : (w1 % 1000 == 128 && d->Co % 128 == 0 ? 128 : 64);
-    const int cot = one ? w1_cot : 64;
+    // 3x3(x3) kw-strip (A/B knob VDIFF_WGRAD3=nst,cot): ring depth and 64 / 128 output
+    // channels per workgroup
+    static const int w3 = [] {
+      const char* e = getenv("VDIFF_WGRAD3");
+      int n = 2, c = 64;
+      if (e) sscanf(e, "%d,%d", &n, &c);
+      return n * 1000 + c;
+    }();
+    const int w3_nst = w3 / 1000, w3_cot = (w3 % 1000 == 128 && d->Co % 128 == 0) ? 128 : 64;
+    const int cot = one ? w1_cot : w3_cot;
     // nine-tap planes (VDIFF_CONV_WPLANE=1, A/B): image rows of whole 64-pixel steps
     static const int wplane = [] {
       const char* e = getenv("VDIFF_CONV_WPLANE");
@@ -1975,6 +1984,15 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     else if (one && w1_nst >= 4) VD_WGD(64, 64, 4, true);
     else if (one) VD_WGD(64, 64, 2, true);
     else if (plane) VD_WGD(224, 64, 2, false, true);
+    else if (cot == 128 && w3_nst >= 3 && rows <= 96) VD_WGD(96, 128, 3, false);
+    else if (cot == 128 && w3_nst >= 3 && rows <= 128) VD_WGD(128, 128, 3, false);
+    else if (cot == 128 && w3_nst >= 3) VD_WGD(192, 128, 3, false);
+    else if (cot == 128 && rows <= 96) VD_WGD(96, 128, 2, false);
+    else if (cot == 128 && rows <= 128) VD_WGD(128, 128, 2, false);
+    else if (cot == 128) VD_WGD(192, 128, 2, false);
+    else if (w3_nst >= 3 && rows <= 96) VD_WGD(96, 64, 3, false);
+    else if (w3_nst >= 3 && rows <= 128) VD_WGD(128, 64, 3, false);
+    else if (w3_nst >= 3) VD_WGD(192, 64, 3, false);
     else if (rows <= 96) VD_WGD(96, 64, 2, false);
     else if (rows <= 128) VD_WGD(128, 64, 2, false);
     else VD_WGD(192, 64, 2, false);
