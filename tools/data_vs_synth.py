@@ -60,11 +60,14 @@ def main():
     ap.add_argument("--clips", type=int, default=8)
     ap.add_argument("--epochs", type=int, default=7)
     ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--lr", default="1e-3",
+                    help="Adam lr of both runs (the reference's 1e-2 drove the random-data run "
+                         "to a non-finite loss near step 50, which Trainer.check_finite reports)")
     a = ap.parse_args()
     d = tempfile.mkdtemp(prefix="vdata_", dir="/tmp")
     index = make_dataset(d, a.clips)
-    synth, ts = run([], a.epochs, a.steps, d)
-    data, td = run(["--data", index], a.epochs, a.steps, d)
+    synth, ts = run(["--lr", a.lr], a.epochs, a.steps, d)
+    data, td = run(["--lr", a.lr, "--data", index], a.epochs, a.steps, d)
     s, r = float(np.mean(synth[1:])), float(np.mean(data[1:]))
     sm, rm = float(np.median(synth[1:])), float(np.median(data[1:]))
     print(json.dumps({"synthetic_frames_per_s": round(s, 3), "data_frames_per_s": round(r, 3),
@@ -72,7 +75,7 @@ def main():
                       "median_synthetic": round(sm, 3), "median_data": round(rm, 3),
                       "median_ratio": round(rm / sm, 4), "epochs_synthetic": synth,
                       "epochs_data": data, "steps_per_epoch": a.steps, "clips": a.clips,
-                      "wall_s": [round(ts, 1), round(td, 1)],
+                      "wall_s": [round(ts, 1), round(td, 1)], "lr": float(a.lr),
                       "workload": "train.py config 2: UNet3D 128x128x16 joint bf16, 1 clip, "
                                   "256x256 uint8 frames + 44.1 kHz audio (.vdclip)"}))
 
