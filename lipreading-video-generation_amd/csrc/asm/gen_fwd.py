@@ -40,7 +40,8 @@ HI = 65536             # ds_read immediates are 16 bits: stages >= 4 use the +64
 NINF, PINF = "0xff800000", "0x7f800000"
 BAR2 = False           # A/B (tools/asm_ab.py): one barrier per two bodies
 CHECK_NOP = 3          # wait states between the check's v_cmp and its branch
-DROP = 0               # timing experiments only (wrong results): 1 exp, 2 add, 4 cvt, 8 reads
+DROP = 0               # timing experiments only (wrong results): 1 exp, 2 add, 4 cvt, 8 reads,
+                       # 16 the loop's LDS-DMA pieces
 CHAINS = 1             # row-sum accumulators per query block (1: one dependent add chain;
                        # 14.24 vs 14.42 ms for 4, profiles/r03_ab_fwd_knobs.txt)
 NORARE = 0             # timing experiment only: never take the rare path (wrong results)
@@ -492,7 +493,7 @@ def emit_body(st: Stream, V, A, u, masked, tag, prev=None):
         put(rslots[2], k_reads(V, A, kst, 1))
         put(rslots[3], tr_reads(V, A, u, 1))
     ops, adv = dma_ops(V, (u + PD) % NST)
-    dma_at = {4: 0, 12: 1, 20: 2, 28: 3}
+    dma_at = {} if DROP & 16 else {4: 0, 12: 1, 20: 2, 28: 3}
     valu = place(softmax_list(V, par, masked, u), nm)
     for g in range(nm):
         if g in dma_at:
