@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--xattn-steps", type=int, default=3,
                     help="timed train steps with audio cross-attention (build extension, "
                          "auxiliary leg); 0 skips it")
+    ap.add_argument("--timer-convs", action="store_true",
+                    help="per-launch conv events inside the timed train steps too (the round-2 "
+                         "measurement; A/B of the events' own cost)")
     ap.add_argument("--c4-steps", type=int, default=3,
                     help="timed DDIM steps at BASELINE config 4 (256x256x25); 0 skips the leg")
     return ap.parse_args()
@@ -471,7 +474,9 @@ def main():
             loss = trainer.step(clip)
             log(f"warmup {i}: loss {float(loss):.4f}")
         barrier_sync(world)
-        timer = ops.KernelTimer()
+        # attention launches only: the roofline's per-launch times (the conv breakdown comes
+        # from one extra untimed step below, so its ~500 event pairs stay out of the timing)
+        timer = ops.KernelTimer(attention=True, convs=args.timer_convs)
         ops.set_timer(timer)
         if trainer.bucketer is not None:
             trainer.bucketer.timing = True
@@ -499,7 +504,11 @@ def main():
             f"model {result['model_tflops_per_gpu']} TFLOP/s/GPU (3x fwd)")
         for r in rows:
             log("  kernel", r)
-        conv = timer.conv_summary()
+        ctimer = ops.KernelTimer(attention=False, convs=True)
+        ops.set_timer(ctimer)
+        trainer.step(clip)  # untimed: per-launch conv times
+        ops.set_timer(None)
+        conv = ctimer.conv_summary()
         by_kind = {}
         for (kind, key), (cnt, tot, flop) in conv.items():
             a = by_kind.setdefault(kind, [0, 0.0, 0.0])
@@ -507,11 +516,12 @@ def main():
             a[1] += tot
             a[2] += flop * cnt
         result["conv_kernels"] = {
-            k: {"launches": c, "ms_per_step": round(t / args.steps, 2),
+            k: {"launches": c, "ms_per_step": round(t, 2),
                 "tflops": round(f / (t / 1e3) / 1e12, 1) if t > 0 else None}
             for k, (c, t, f) in sorted(by_kind.items())}
+        result["conv_kernels"]["note"] = "one extra untimed train step after the timed ones"
         for (kind, key), (cnt, tot, flop) in sorted(conv.items(), key=lambda kv: -kv[1][1])[:60]:
-            log(f"  conv {kind:16s} {key:40s} x{cnt // args.steps:<3d} {tot / args.steps:7.2f} ms/step "
+            log(f"  conv {kind:16s} {key:40s} x{cnt:<3d} {tot:7.2f} ms/step "
                 f"{flop * cnt / (tot / 1e3) / 1e12:7.1f} TF/s")
         del trainer
         torch.cuda.empty_cache()

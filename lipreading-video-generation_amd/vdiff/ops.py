@@ -648,7 +648,7 @@ class ConvFn(torch.autograd.Function):
             if list(res.shape) != ys:
                 raise ValueError(f"residual shape {list(res.shape)} != output {ys}")
         d = _desc(B, sp, Cip, out, Co, k, s, p, _DT[dt])
-        ev = _timer.begin() if _timer is not None else None
+        ev = _timer.begin() if _timer is not None and _timer.convs else None
         _lib.call("vd_conv3d_fwd", d, _p(xp), _p(w_fwd), _p(b32), _p(ca), _p(res), _p(y),
                   _stream(x))
         if ev is not None:
@@ -680,7 +680,7 @@ class ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             w_bwd = _pack_weight(weight, Co, Ci, taps, Cip, Cop, True, dt)
             dxp = empty_cl([B, Cip] + xshape[2:], dt, dy.device)
-            ev = _timer.begin() if _timer is not None else None
+            ev = _timer.begin() if _timer is not None and _timer.convs else None
             if dt == torch.bfloat16 and any(v > 1 for v in s):
                 # Strided conv (Downsample): dX of a stride-s conv = dX of the stride-1 conv
                 # of the same taps and padding whose dY is zero everywhere except at the
@@ -700,7 +700,7 @@ class ConvFn(torch.autograd.Function):
             dx = dxp[:, :Ci] if Cip != Ci else dxp
         if ctx.needs_input_grad[1]:
             dwp = torch.zeros(Cop, taps, Cip, dtype=torch.float32, device=dy.device)
-            ev = _timer.begin() if _timer is not None else None
+            ev = _timer.begin() if _timer is not None and _timer.convs else None
             _lib.call("vd_conv3d_bwd_weight", d, _p(xp), _p(dyp), _p(dwp), st)
             if ev is not None:
                 _timer.end_conv(ev, "conv_bwd_weight", _conv_key(Cip, Co, k, s, out),
@@ -730,12 +730,16 @@ def conv(x, weight, bias=None, stride=1, padding=0, chan_add=None, residual=None
 
 # --------------------------------------------------------------- Attention
 class KernelTimer:
-    """HIP-event timing of every flash-attention launch on the launching (current) stream.
+    """HIP-event timing of every flash-attention launch (attention=True) and every
+    implicit-GEMM conv launch (convs=True) on the launching (current) stream.
 
-    bench.py installs one over its timed region: vdiff.ops.set_timer(KernelTimer()).
+    bench.py installs an attention-only timer over its timed region (the roofline needs the
+    attention launch times; ~500 conv event pairs per step would add their own packets to
+    the timed step) and a conv-only timer over one extra, untimed step.
     Each record is (kind, head_dim, seq_len, nseq, start_event, end_event)."""
 
-    def __init__(self):
+    def __init__(self, attention=True, convs=True):
+        self.attention, self.convs = attention, convs
         self.records = []
         self.conv_records = []  # (kind, geometry key, flop, start, end): implicit-GEMM convs
 
@@ -837,7 +841,7 @@ class AttentionFn(torch.autograd.Function):
             base = qkv.data_ptr()
             nws = _lib.lib().vd_attention_fwd_workspace_size(d)  # KV-split partials, or 0
             ws = torch.empty(nws, dtype=torch.uint8, device=qkv.device) if nws else None
-            ev = _timer.begin() if _timer is not None else None
+            ev = _timer.begin() if _timer is not None and _timer.attention else None
             _lib.call("vd_attention_fwd_ws", d, base + qo * es, base + ko * es, base + vo * es,
                       out.data_ptr() + oo * es, _p(lse), _p(ws), nws, _stream(qkv))
             if ev is not None:
@@ -864,7 +868,7 @@ class AttentionFn(torch.autograd.Function):
             ws = torch.empty(max(1, _lib.lib().vd_attention_bwd_workspace_size(d)),
                              dtype=torch.uint8, device=qkv.device)
             st = _stream(qkv)
-            ev = _timer.begin() if _timer is not None else None
+            ev = _timer.begin() if _timer is not None and _timer.attention else None
             _lib.call("vd_attention_bwd_dq", d, base + qo * es, base + ko * es, base + vo * es,
                       obase + oo * es, dobase + oo * es, _p(lse), dbase + qo * es, _p(ws), st)
             if ev is not None:
