@@ -489,6 +489,10 @@ class step_packed_weights:
 
     def __enter__(self):
         global _step_pack
+        if self.plans and any(spec[0].data_ptr() != k[1] for k, spec in self.want.items()):
+            # a planned weight's storage moved or was freed since the plan was built (.to(),
+            # load_state_dict(assign=True), .data = ...): never read the old pointer
+            self.bufs, self.plans, self.dirty = {}, [], True
         if self.plans:
             for dt, table, n, total in self.plans:
                 _lib.call("vd_conv_pack_weights", _p(table), n, total, _DT[dt], _stream(table))

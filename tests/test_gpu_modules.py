@@ -378,3 +378,21 @@ def test_trainer_batched_pack_equals_per_call_pack():
     assert rel_l2(runs[1][0], runs[0][0]) < 1e-5
     for a, b in zip(runs[0][1], runs[1][1]):
         assert rel_l2(b, a) < 1e-5
+
+
+def test_batched_pack_plan_survives_moved_weights():
+    """A weight whose storage is replaced between steps (here .data = a new tensor) drops
+    the batched-pack plan before its launch (the old pointer is never read) and the step
+    still packs the current weights: the conv output equals a fresh per-call pack's."""
+    from vdiff import ops
+    w = torch.nn.Parameter(torch.randn(64, 32, 3, 3, 3, device=dev) * 0.05)
+    x = ops.to_cl(torch.randn(1, 32, 4, 16, 16, device=dev).bfloat16())
+    sp = ops.step_packed_weights()
+    with sp:
+        ops.conv(x, w, padding=1)
+    assert sp.dirty is False and sp.plans  # plan built at the end of the first step
+    w.data = torch.randn_like(w) * 0.05      # new storage
+    with sp:
+        y = ops.conv(x, w, padding=1)
+    y0 = ops.conv(x, w, padding=1)          # no plan: per-call pack
+    assert torch.equal(y, y0)
