@@ -5,6 +5,9 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 T=${1:-r03g}
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_gpu_modules.py -k pack > gpurun_out/${T}_pack_tests.log 2>&1; rc=$?
+tail -1 gpurun_out/${T}_pack_tests.log; case $rc in 0|1) ;; *) exit $rc ;; esac
 for i in 1 2; do
   for f in "" "--timer-convs"; do
     timeout -k 10 300 python -u bench.py --only train --no-cpu --steps 5 --warmup 2 $f \
