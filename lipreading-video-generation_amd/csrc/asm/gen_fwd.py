@@ -47,6 +47,9 @@ CHAINS = 1             # row-sum accumulators per query block (1: one dependent 
 NORARE = 0             # timing experiment only: never take the rare path (wrong results)
 STAMP = 0              # diagnostic: store loop cycles / realtime per workgroup (karg 112)
 GSGS = 0               # MFMA order of a body: 0 G(kb0) G(kb1) S(kb0) S(kb1); 1 G S G S
+LAG1 = 0               # CHAINS = 1 through the lagged list (adds 4 scores behind their exps)
+DMAS = 0               # LDS-DMA slots of a body: 0 {4,12,20,28} 1 {1,9,17,25} 2 {6,14,22,30}
+                       # 3 {0,8,16,24}
 MSUM = 0               # row sums on the matrix pipe: 8 MFMAs (ones x P^T) per body replace the
                        # 64 v_add_f32; the tile's lagged-max check moves to the next body's top
 
@@ -179,7 +182,7 @@ def softmax_list(V, par, masked, u):
                         out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + kk)}, v{S + 2 * kk}, "
                                     f"v{S + 2 * kk + 1}", COST["cvt"], gk[kb]))
         return [it for it in out if not DROP & kinds.get(it[0].split()[0], 0)]
-    if CHAINS == 1:
+    if CHAINS == 1 and not LAG1:
         for kb in range(2):
             for j in range(2):
                 p = 2 * kb + j
@@ -493,7 +496,8 @@ def emit_body(st: Stream, V, A, u, masked, tag, prev=None):
         put(rslots[2], k_reads(V, A, kst, 1))
         put(rslots[3], tr_reads(V, A, u, 1))
     ops, adv = dma_ops(V, (u + PD) % NST)
-    dma_at = {} if DROP & 16 else {4: 0, 12: 1, 20: 2, 28: 3}
+    slots4 = ((4, 12, 20, 28), (1, 9, 17, 25), (6, 14, 22, 30), (0, 8, 16, 24))[DMAS]
+    dma_at = {} if DROP & 16 else {g: i for i, g in enumerate(slots4)}
     valu = place(softmax_list(V, par, masked, u), nm)
     for g in range(nm):
         if g in dma_at:
