@@ -230,16 +230,26 @@ def softmax_list(V, par, masked, u):
                 out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * p + k)}, v{S + r - 1}, v{S + r}",
                             COST["cvt"], gk[kb]))
     # combine the accumulators of each query block into ps
-    for j in range(2):
-        out.append((f"v_add_f32 {V.r('c', 4 * j)}, {V.r('c', 4 * j)}, {V.r('c', 4 * j + 1)}",
-                    COST["add"], 0))
-    for j in range(2):
-        out.append((f"v_add_f32 {V.r('c', 4 * j + 2)}, {V.r('c', 4 * j + 2)}, "
-                    f"{V.r('c', 4 * j + 3)}", COST["add"], 0))
-    for j in range(2):
-        out.append((f"v_add_f32 {V.r('ps', j)}, {V.r('c', 4 * j)}, {V.r('c', 4 * j + 2)}",
-                    COST["add"], 0))
+    out += combine_list(V)
     return [it for it in out if not DROP & kinds.get(it[0].split()[0], 0)]
+
+
+def combine_list(V):
+    """The CHAINS row-sum accumulators of each query block into ps (a pairwise tree)."""
+    out = []
+    if CHAINS == 1:
+        return [(f"v_mov_b32 {V.r('ps', j)}, {V.r('c', 4 * j)}", COST["add"], 0)
+                for j in range(2)]
+    step = 1
+    while step < CHAINS:
+        last = 2 * step >= CHAINS
+        for a in range(0, CHAINS, 2 * step):
+            for j in range(2):
+                dst = V.r("ps", j) if last else V.r("c", 4 * j + a)
+                out.append((f"v_add_f32 {dst}, {V.r('c', 4 * j + a)}, "
+                            f"{V.r('c', 4 * j + a + step)}", COST["add"], 0))
+        step *= 2
+    return out
 
 
 def mask_list(V, S, masked, u, kb):

@@ -36,6 +36,8 @@ HI = 65536
 NINF, PINF = "0xff800000", "0x7f800000"
 CHECK_NOP = 3
 CHAINS = 4
+DMAS = 0               # LDS-DMA slots of a body (A/B): 0 {4,12,20,28} 1 {1,9,17,25} 2 {6,14,22,30}
+KSLOT = 0              # first gap of the K(t+1) row reads (one per gap)
 
 S_KARG = "s[0:1]"
 S_WGX, S_WGY, S_WGZ = "s2", "s3", "s4"
@@ -179,15 +181,25 @@ def softmax_list(V, par, masked, u):
                 k = r // 2
                 out.append((f"v_cvt_pk_bf16_f32 {V.r('p', 8 * j + k)}, v{S + r - 1}, v{S + r}",
                             COST["cvt"], 16 + 2 * (k // 4) + j))
-    for j in range(2):
-        out.append((f"v_add_f32 {V.r('c', 4 * j)}, {V.r('c', 4 * j)}, {V.r('c', 4 * j + 1)}",
-                    COST["add"], 0))
-    for j in range(2):
-        out.append((f"v_add_f32 {V.r('c', 4 * j + 2)}, {V.r('c', 4 * j + 2)}, "
-                    f"{V.r('c', 4 * j + 3)}", COST["add"], 0))
-    for j in range(2):
-        out.append((f"v_add_f32 {V.r('ps', j)}, {V.r('c', 4 * j)}, {V.r('c', 4 * j + 2)}",
-                    COST["add"], 0))
+    out += combine_list(V)
+    return out
+
+
+def combine_list(V):
+    """The CHAINS row-sum accumulators of each query block into ps (a pairwise tree)."""
+    out = []
+    if CHAINS == 1:
+        return [(f"v_mov_b32 {V.r('ps', j)}, {V.r('c', 4 * j)}", COST["add"], 0)
+                for j in range(2)]
+    step = 1
+    while step < CHAINS:
+        last = 2 * step >= CHAINS
+        for a in range(0, CHAINS, 2 * step):
+            for j in range(2):
+                dst = V.r("ps", j) if last else V.r("c", 4 * j + a)
+                out.append((f"v_add_f32 {dst}, {V.r('c', 4 * j + a)}, "
+                            f"{V.r('c', 4 * j + a + step)}", COST["add"], 0))
+        step *= 2
     return out
 
 
@@ -381,10 +393,10 @@ def emit_body(st: Stream, V, A, u, masked, tag):
             reads.setdefault(slot0 + k // per, []).append(item)
 
     kst = (u + 1) % NST
-    put(0, k_reads(V, A, kst), 1)     # K(t+1) rows: gaps 0..7, read by S(t+1) from gap 16
+    put(KSLOT, k_reads(V, A, kst), 1)  # K(t+1) rows: gaps 0..7, read by S(t+1) from gap 16
     put(16, tr_reads(V, A, u), 2)     # V(t)^T for G(t) in the next body: gaps 16..23
     ops, adv = dma_ops(V, (u + PD) % NST)
-    dma_at = {4: 0, 12: 1, 20: 2, 28: 3}
+    dma_at = {g: i for i, g in enumerate(((4, 12, 20, 28), (1, 9, 17, 25), (6, 14, 22, 30))[DMAS])}
     valu = place(softmax_list(V, par, masked, u), nm)
     for g in range(nm):
         if g in dma_at:

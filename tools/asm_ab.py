@@ -19,8 +19,14 @@ sys.path.insert(0, os.path.join(ROOT, "lipreading-video-generation_amd"))
 import torch  # noqa: E402
 
 import gen_attn_asm as G  # noqa: E402
-import gen_fwd as F  # noqa: E402
+import gen_fwd as F64  # noqa: E402
+import gen_fwd128 as F128  # noqa: E402
 from asmgen import code_object_text  # noqa: E402
+
+D128 = "--d128" in sys.argv  # the head_dim-128 forward (gen_fwd128 knobs), N = 65536
+if D128:
+    sys.argv.remove("--d128")
+F = F128 if D128 else F64
 
 hip = C.CDLL("libamdhip64.so.7")
 
@@ -35,15 +41,20 @@ def build(knobs):
     for k, v in knobs.items():
         setattr(F, k, v)
     try:
-        kfw, _ = F.gen_fwd()
-        _, ddq, _ = G.gen_dq()
+        if D128:
+            kfw, dfw, _ = F.gen_fwd128()
+        else:
+            kfw, _ = F.gen_fwd()
     finally:
         for k, v in saved.items():
             setattr(F, k, v)
     d = tempfile.mkdtemp()
     s, o, co = (os.path.join(d, x) for x in ("f.s", "f.o", "f.hsaco"))
-    kdq, _, _ = G.gen_dq()
-    open(s, "w").write(code_object_text([kdq, kfw], ddq))
+    if D128:
+        open(s, "w").write(code_object_text([kfw], dfw))
+    else:
+        kdq, ddq, _ = G.gen_dq()
+        open(s, "w").write(code_object_text([kdq, kfw], ddq))
     subprocess.run(["/opt/rocm/llvm/bin/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
                     "-mcpu=gfx950", "-c", s, "-o", o], check=True)
     subprocess.run(["/opt/rocm/llvm/bin/ld.lld", "-shared", o, "-o", co], check=True)
@@ -51,7 +62,8 @@ def build(knobs):
     mod, fn = C.c_void_p(), C.c_void_p()
     buf = C.create_string_buffer(blob, len(blob))
     check(hip.hipModuleLoadData(C.byref(mod), buf), "load")
-    check(hip.hipModuleGetFunction(C.byref(fn), mod, b"vd_attn_fwd_d64"), "function")
+    name = b"vd_attn_fwd_d128" if D128 else b"vd_attn_fwd_d64"
+    check(hip.hipModuleGetFunction(C.byref(fn), mod, name), "function")
     return fn, buf
 
 
@@ -66,7 +78,8 @@ def launch(fn, args: bytes, grid):
 
 def main():
     from vdiff import ops
-    N, C3, D = 262144, 192, 64
+    N, C3, D = (65536, 384, 128) if D128 else (262144, 192, 64)
+    TR = 32 if D128 else 64  # keys per tile; 8 tiles per iteration
     torch.manual_seed(0)
     qkv_t = (torch.randn(N, C3, device="cuda") * 1.3).bfloat16()   # token-major
     qkv = qkv_t.T.unsqueeze(0)                                      # [1, 192, N] channels-last view
@@ -74,13 +87,13 @@ def main():
     refo = ref[0].T.float()
     o = torch.empty(N, D, device="cuda", dtype=torch.bfloat16)
     lse = torch.empty(N, device="cuda", dtype=torch.float32)
-    niter = math.ceil(N / 512)
+    niter = math.ceil(N / (8 * TR))
     ts_b, ots_b = C3 * 2, D * 2
-    args = struct.pack("<5Q4I4Qf5I", qkv_t.data_ptr(), qkv_t.data_ptr() + 128,
-                       qkv_t.data_ptr() + 256, o.data_ptr(), lse.data_ptr(), N, ts_b, ots_b, 1,
+    args = struct.pack("<5Q4I4Qf5I", qkv_t.data_ptr(), qkv_t.data_ptr() + 2 * D,
+                       qkv_t.data_ptr() + 4 * D, o.data_ptr(), lse.data_ptr(), N, ts_b, ots_b, 1,
                        0, 0, 0, 0, (1 / math.sqrt(D)) * 1.4426950408889634,
-                       ((N - 1) * C3 + 64) * 2, ((N - 1) * D + 64) * 2, 64 * ts_b, niter,
-                       N - 512 * (niter - 1))
+                       ((N - 1) * C3 + D) * 2, ((N - 1) * D + D) * 2, TR * ts_b, niter,
+                       N - 8 * TR * (niter - 1))
     flops = 4 * N * N * D
     for spec in sys.argv[1:]:
         name, _, kv = spec.partition(":")
