@@ -36,6 +36,9 @@ NST = 4
 KARG = 144              # AsmDkdvArgs (vd_asm.h)
 START = 17
 HI = 65536
+# read / DMA placement knobs (A/B, tools/asm_ab_bwd128.py): first gap of each read group
+DK_TR0, DK_ROW1, DK_TR1 = 1, 18, 32
+DK_DMA0 = 49
 
 # SGPRs (kernel arguments in s[16:51], see gen_attn_asm.py dK/dV map)
 S_KARG = "s[0:1]"
@@ -361,11 +364,11 @@ def emit_iter(st: Stream, V, A, stage, vlist):
         for k, (text, rid) in enumerate(lst):
             slots.setdefault(slot0 + k // per, []).insert(0 if per == 1 else k % per, (text, rid))
 
-    put(1, tr_reads(V, A, prev, 1))       # G(t-1, qb1) operands, tile t-1: slots 1..16
-    put(18, row_reads(V, A, stage, 1))    # (t, qb1) fragments: 18..29
-    put(32, tr_reads(V, A, stage, 0))     # G(t, qb0) operands: 32..47
+    put(DK_TR0, tr_reads(V, A, prev, 1))     # G(t-1, qb1) operands, tile t-1: slots 1..16
+    put(DK_ROW1, row_reads(V, A, stage, 1))  # (t, qb1) fragments: 18..29
+    put(DK_TR1, tr_reads(V, A, stage, 0))    # G(t, qb0) operands: 32..47
     ops, adv = dma_ops(V, prev)
-    dma_at = [49, 50, 51, 52, 53, 54, 55, 56, 57]
+    dma_at = list(range(DK_DMA0, DK_DMA0 + 9))
     for g in range(nm):
         if g == 48:
             st.raw("s_waitcnt vmcnt(9) lgkmcnt(0)")
@@ -455,6 +458,8 @@ def gen_dkdv128():
 # LDS-DMA pieces per wave), one barrier per tile behind s_waitcnt vmcnt(8).
 DQ_KARG = 128
 DQ_START = 26
+DQ_KV0, DQ_TR0, DQ_KV1, DQ_TR1 = 0, 8, 16, 32   # read placement knobs (A/B)
+DQ_DMA = (2, 5, 8, 11, 14, 17, 20, 23)
 RQ3, RK3, RV3, RO3, RL3, RD3, RDQ3 = ("s[56:59]", "s[60:63]", "s[64:67]", "s[68:71]",
                                       "s[72:75]", "s[76:79]", "s[80:83]")
 S3_WAVE, S3_Q0, S3_M0, S3_ITER = "s84", "s85", "s86", "s87"
@@ -688,12 +693,12 @@ def dq_emit_tile(st: Stream, V, A, stage, vlist):
         for k, (text, rid) in enumerate(lst):
             slots.setdefault(slot0 + k // per, []).insert(k % per, (text, rid))
 
-    put(0, dq_kv_reads(V, A, stage, 0))    # kb0 rows: slots 0..7 (consumed 8..23)
-    put(8, dq_tr_reads(V, stage, 0))       # K^T kb0 of this tile, for the next G: 8..15
-    put(16, dq_kv_reads(V, A, stage, 1))   # kb1 rows: 16..23 (consumed 32..47)
-    put(32, dq_tr_reads(V, stage, 1))      # K^T kb1: 32..39
+    put(DQ_KV0, dq_kv_reads(V, A, stage, 0))  # kb0 rows: slots 0..7 (consumed 8..23)
+    put(DQ_TR0, dq_tr_reads(V, stage, 0))     # K^T kb0 of this tile, for the next G: 8..15
+    put(DQ_KV1, dq_kv_reads(V, A, stage, 1))  # kb1 rows: 16..23 (consumed 32..47)
+    put(DQ_TR1, dq_tr_reads(V, stage, 1))     # K^T kb1: 32..39
     ops, adv = dq_dma_ops(V, (stage + 2) % NST)
-    dma_at = [2, 5, 8, 11, 14, 17, 20, 23]
+    dma_at = list(DQ_DMA)
     # the G products read the K^T fragments of the previous tile (no LDS wait of their own)
     mf = [(t, ()) if k < 8 or 24 <= k < 32 else (t, d) for k, (t, d) in enumerate(mf)]
     for g in range(nm):
