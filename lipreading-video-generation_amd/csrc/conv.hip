@@ -1939,13 +1939,14 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
                                              : (w1 % 1000 == 128 && d->Co % 128 == 0 ? 128 : 64);
     // 3x3(x3) kw-strip (A/B knob VDIFF_WGRAD3=nst,cot): ring depth and 64 / 128 output
     // channels per workgroup
-    static const int w3 = [] {
+    static const int w3 = [] {  // nst,cot[,pixels per split / 64]
       const char* e = getenv("VDIFF_WGRAD3");
-      int n = 2, c = 64;
-      if (e) sscanf(e, "%d,%d", &n, &c);
-      return n * 1000 + c;
+      int n = 2, c = 64, m = 32;
+      if (e) sscanf(e, "%d,%d,%d", &n, &c, &m);
+      return m * 1000000 + n * 1000 + c;
     }();
-    const int w3_nst = w3 / 1000, w3_cot = (w3 % 1000 == 128 && d->Co % 128 == 0) ? 128 : 64;
+    const int w3_nst = w3 / 1000 % 1000, w3_msteps = w3 / 1000000;
+    const int w3_cot = (w3 % 1000 == 128 && d->Co % 128 == 0) ? 128 : 64;
     const int cot = one ? w1_cot : w3_cot;
     // nine-tap planes (VDIFF_CONV_WPLANE=1, A/B): image rows of whole 64-pixel steps
     static const int wplane = [] {
@@ -1960,7 +1961,7 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     // occupancy: 64->64 at 128x128 0.13 -> 0.116 ms, tools/conv_ab.sh); planes do three
     // times the MFMA work per step: at least 16 steps
     int64_t splits = vd_cdiv(2048, tiles);
-    int64_t maxs = vd_cdiv(g.M, (one || plane) ? 1024 : 2048);
+    int64_t maxs = vd_cdiv(g.M, (one || plane) ? 1024 : 64 * w3_msteps);
     if (splits > maxs) splits = maxs;
     if (splits < 1) splits = 1;
     g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
