@@ -1,0 +1,51 @@
+"""GroupNorm(32)+SiLU forward and backward (vd_groupnorm_silu_fwd/_bwd through
+ops.group_norm_silu) at the UNet3D 128x128x16 shapes, bf16, timed with HIP events; GB/s
+counts the algorithmic bytes (fwd: x read twice + y written; bwd: x and dy read twice +
+dx written)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "lipreading-video-generation_amd"))
+
+import torch  # noqa: E402
+
+from vdiff import ops  # noqa: E402
+
+# (channels, frames, H = W)
+SHAPES = ((64, 16, 128), (128, 16, 128), (192, 16, 128), (128, 16, 64), (256, 16, 64),
+          (384, 16, 64), (256, 16, 32), (512, 16, 32), (768, 16, 32))
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    for C, T, H in SHAPES:
+        x = ops.to_cl(torch.randn(1, C, T, H, H, device="cuda").bfloat16()).requires_grad_(True)
+        w = torch.randn(C, device="cuda", requires_grad=True)
+        b = torch.randn(C, device="cuda", requires_grad=True)
+        g = ops.to_cl(torch.randn(1, C, T, H, H, device="cuda").bfloat16())
+        size = x.numel() * 2
+        fwd = timeit(lambda: ops.group_norm_silu(x.detach(), w.detach(), b.detach()))
+        y = ops.group_norm_silu(x, w, b)
+
+        def bwd():
+            torch.autograd.grad(y, (x, w, b), g, retain_graph=True)
+
+        full = timeit(bwd)
+        print(f"GN+SiLU C={C:4d} {T}x{H}x{H}: fwd {fwd:7.1f} us ({3 * size / fwd / 1e3:6.0f} GB/s)"
+              f"  bwd {full:7.1f} us ({5 * size / full / 1e3:6.0f} GB/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

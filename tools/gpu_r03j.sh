@@ -10,3 +10,6 @@ for v in 2,64,32 2,64,16 2,128,16 2,128,8 3,128,16 2,64,32 2,64,24 2,128,24; do
   grep "per train step" gpurun_out/${T}_wgrad3.txt | tail -1
   case $rc in 0|1) ;; *) exit $rc ;; esac
 done
+timeout -k 10 300 python -u tools/gn_bench.py > gpurun_out/${T}_gn.txt 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/${T}_gn.txt | tail -10
+exit $rc
