@@ -12,8 +12,8 @@ softmax.  Per 64-query tile (2 query blocks qb) a wave runs 64 v_mfma_f32_32x32x
 the order
     S/dP(t, qb0) [16] | G(t-1, qb1) [16] | S/dP(t, qb1) [16] | barrier | G(t, qb0) [16]
 (G = 8 dV + 8 dK products: 4 output-dim blocks x 2 query k-steps), 96 VALU instructions (32
-v_exp_f32, 32 v_mul_f32, 32 v_cvt_pk_bf16_f32) placed at a constant rate from gap START, 56
-LDS fragment reads (24 ds_read_b128, 32 ds_read_b64_tr_b16 pairs) and 9 LDS-DMA pieces.
+v_exp_f32, 32 v_mul_f32, 32 v_cvt_pk_bf16_f32) placed at a constant rate from gap START, 112
+LDS fragment reads (48 ds_read_b128, 64 ds_read_b64_tr_b16) and 9 LDS-DMA pieces.
 
 LDS: the row constants (-lse', -delta: 4 x 768 B, as the D = 64 kernel) then a 4-stage ring
 of (Q tile 16 KiB | dO tile 16 KiB) = 131 KiB, tile t + 3 issued after the barrier of tile

@@ -1,0 +1,76 @@
+"""CPU checks of the hand-scheduled kernel generators (csrc/asm/): the code object the
+library embeds assembles for gfx950, every kernel fits the 512-entry register file at one
+wave per SIMD, and each body's instruction mix is the one the generator documents (MFMAs
+per tile, no padding nops inside the MFMA streams beyond the counted hazards).  No GPU."""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+ASM = os.path.join(ROOT, "lipreading-video-generation_amd", "csrc", "asm")
+CLANG = "/opt/rocm/llvm/bin/clang"
+
+
+@pytest.fixture(scope="module")
+def gens():
+    sys.path.insert(0, ASM)
+    try:
+        import gen_attn_asm as G
+        import gen_d128 as D128
+        import gen_fwd as F64
+        import gen_fwd128 as F128
+        yield G, F64, D128, F128
+    finally:
+        sys.path.remove(ASM)
+
+
+def test_code_object_assembles(tmp_path, gens):
+    if not shutil.which(CLANG) and not os.path.exists(CLANG):
+        pytest.skip("ROCm clang not present")
+    out = tmp_path / "attn_asm.s"
+    subprocess.run([sys.executable, os.path.join(ASM, "gen_attn_asm.py"), str(out)], check=True)
+    text = out.read_text()
+    for name in ("vd_attn_bwd_dq_d64", "vd_attn_bwd_dkdv_d64", "vd_attn_fwd_d64",
+                 "vd_attn_bwd_dkdv_d128", "vd_attn_bwd_dq_d128", "vd_attn_fwd_d128"):
+        assert f".amdhsa_kernel {name}" in text, name
+    subprocess.run([CLANG, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
+                    "-c", str(out), "-o", str(tmp_path / "a.o")], check=True)
+
+
+def test_register_budgets(gens):
+    G, F64, D128, F128 = gens
+    for regs in (G.regs_dq, G.regs_dkdv, F64.regs, D128.regs, D128.dq_regs, F128.regs):
+        V, A = regs()
+        assert V.next <= 256 and A.next <= 256, (regs, V.next, A.next)
+        assert (V.next + 3) // 4 * 4 + A.next <= 512
+
+
+def _body_counts(lines, start, stop):
+    i0 = next(i for i, l in enumerate(lines) if start in l)
+    i1 = next(i for i, l in enumerate(lines) if i > i0 and stop in l)
+    ops = [l.split()[0] for l in lines[i0:i1] if l.strip() and not l.strip().startswith((";", "."))]
+    return {k: ops.count(k) for k in set(ops)}
+
+
+def test_instruction_mix_per_tile(gens):
+    G, F64, D128, F128 = gens
+    mf = "v_mfma_f32_32x32x16_bf16"
+    _, _, st = D128.gen_dkdv128()
+    c = _body_counts(st.lines, "query tile, ring stage 1", "query tile, ring stage 2")
+    assert c[mf] == 64 and c["v_exp_f32"] == 32 and c["ds_read_b64_tr_b16"] == 64
+    assert c["ds_read_b128"] == 48
+    assert c["buffer_load_dwordx4"] == 8 and c["buffer_load_dword"] == 1
+    _, st = D128.gen_dq128()
+    c = _body_counts(st.lines, "key tile, ring stage 1", "key tile, ring stage 2")
+    assert c[mf] == 48 and c["v_exp_f32"] == 32 and c["buffer_load_dwordx4"] == 8
+    _, _, st = F128.gen_fwd128()
+    c = _body_counts(st.lines, "body, stage 1", "body, stage 2")
+    assert c[mf] == 32 and c["v_exp_f32"] == 32 and c["v_cvt_pk_bf16_f32"] == 16
+    _, st = F64.gen_fwd()
+    c = _body_counts(st.lines, "body, stage 1", "body, stage 2")
+    assert c[mf] == 32 and c["v_exp_f32"] == 64 and c["v_cvt_pk_bf16_f32"] == 32
+    assert c.get("s_nop", 0) <= 8
