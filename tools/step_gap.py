@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lr", type=float, default=1e-2, help="0 keeps the weights fixed")
+    ap.add_argument("--no-timer", action="store_true",
+                    help="no per-launch attention events (for a kernel trace: tools/idle_gaps.py)")
     a = ap.parse_args()
     args = argparse.Namespace(size=128, frames=16, dtype="bf16", mode="joint")
     dev = torch.device("cuda", 0)
@@ -48,16 +50,17 @@ def main():
     clip = synthetic_clip(1, 16, 128, 100, dev, seed=0)
     tr.step(clip)  # warm-up: state, tables, packed weights
     torch.cuda.synchronize()
+    torch.cuda._sleep(1000)  # trace marker (spin kernel): the timed rounds start after it
     ps, gs = [], []
     for r in range(a.rounds):
-        timer = ops.KernelTimer()
+        timer = ops.KernelTimer() if not a.no_timer else None
         ops.set_timer(timer)
         p, g = run(tr, clip, a.steps)
         ops.set_timer(None)
         ps.extend(p)
         gs.extend(g)
         per = {}
-        for (kind, hd, n, nseq), (cnt, ms) in timer.summary().items():
+        for (kind, hd, n, nseq), (cnt, ms) in (timer.summary().items() if timer else ()):
             per[(kind, hd)] = per.get((kind, hd), 0.0) + ms / a.steps
         print(f"round {r} period " + " ".join(f"{x:.2f}" for x in p)
               + " | boundary gap " + " ".join(f"{x:.3f}" for x in g), flush=True)
