@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--after", default="spin",
                     help="start after the last kernel whose name contains this (a marker)")
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=1, help="divide the per-kernel totals by this")
     a = ap.parse_args()
     paths = [q for p in a.paths for q in (glob.glob(p, recursive=True) or [p])]
     rows = load(paths)
@@ -56,6 +57,13 @@ def main():
               f"{sum(g) / 1e6:8.3f} ms")
     for d, p, n in sorted(gaps, reverse=True)[:a.top]:
         print(f"  {d / 1e3:9.1f} us  after {(p or '')[:60]}  before {n[:60]}")
+    per = {}
+    for s, e, n in rows:
+        c, t = per.get(n, (0, 0))
+        per[n] = (c + 1, t + e - s)
+    print(f"kernel time per step ({a.steps} steps in the window):")
+    for n, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:3 * a.top]:
+        print(f"  {t / 1e6 / a.steps:9.3f} ms  {c / a.steps:7.1f} launches  {n[:90]}")
 
 
 if __name__ == "__main__":
