@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--xattn-steps", type=int, default=3,
                     help="timed train steps with audio cross-attention (build extension, "
                          "auxiliary leg); 0 skips it")
+    ap.add_argument("--no-train-graph", dest="train_graph", action="store_false",
+                    help="skip the auxiliary graph-replayed train-step leg")
     ap.add_argument("--timer-convs", action="store_true",
                     help="per-launch conv events inside the timed train steps too (the round-2 "
                          "measurement; A/B of the events' own cost)")
@@ -391,6 +393,38 @@ def xattn_leg(args, rank, world, device, base_ms):
     return out
 
 
+def graph_leg(args, device, base_ms):
+    """Auxiliary (one process): the same train step with the denoiser's forward + backward
+    replayed as one HIP graph (Trainer(graph=True), vdiff.engine.TrainStepGraph; wav2vec2 and
+    Adam eager around it), from a fresh model of the same init: max(3, warmup) untimed steps
+    (two eager, the capture), then --steps timed replays.  The headline `value` stays the
+    eager step, whose per-launch attention events the roofline needs."""
+    from vdiff.engine import Trainer, synthetic_clip
+    from vdiff.schedulers import LinearNoiseScheduler
+    torch.manual_seed(1234)
+    model = build_model(args, device)
+    tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2, graph=True)
+    clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=0)
+    for _ in range(max(3, args.warmup)):
+        tr.step(clip)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.step(clip)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = el / args.steps * 1e3
+    out = {"metric": "train-step frames/sec, denoiser fwd+bwd as one HIP graph",
+           "value": round(args.clips_per_gpu * args.frames * args.steps / el, 4),
+           "unit": "frames/s", "ms_per_step": round(ms, 2),
+           "ms_vs_eager": round(ms - base_ms, 2) if base_ms else None,
+           "loss": round(float(loss), 4)}
+    log(f"train graph: {ms:.1f} ms/step")
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def free_port():
     import socket
     s = socket.socket()
@@ -588,6 +622,13 @@ def main():
         except Exception as e:
             log(f"xattn leg failed: {type(e).__name__}: {e}")
             result["audio_xattn"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
+
+    if args.only in ("train", "all") and args.train_graph and world == 1:
+        try:  # an auxiliary leg: never let it take the headline numbers down
+            result["train_graph"] = graph_leg(args, device, result.get("ms_per_step"))
+        except Exception as e:
+            log(f"train graph leg failed: {type(e).__name__}: {e}")
+            result["train_graph"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
 
     if args.only in ("vivit", "all") and args.vivit_steps > 0:
         try:  # an auxiliary leg: never let it take the headline numbers down

@@ -116,6 +116,13 @@ int vd_ddim_step(const void* xt, const void* eps, const void* z, void* x_prev,
  * ResBlock.out_layers (unet.py:218-225): element i is kept with probability
  * 1 - drop_p (scaled by 1/(1-drop_p)) by a counter-based hash of (seed, i);
  * the backward regenerates the same mask from the same seed. */
+/* counter (device memory, or NULL = off): while set, every GroupNorm launch
+ * with drop_p > 0 also takes this pointer and mixes the uint64 it reads at run
+ * time into its seed.  A train step captured as a HIP graph (vdiff.engine.
+ * Trainer(graph=True)) freezes the host seed in the launch arguments; bumping
+ * the counter before each replay gives every step a fresh mask, the forward
+ * and backward of one step the same one.  Host-side setting; no GPU call. */
+void vd_set_dropout_counter(const uint64_t* counter);
 size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G);
 int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta,
                           void* y, float* mean, float* rstd, int B, int64_t S,

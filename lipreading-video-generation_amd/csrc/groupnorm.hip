@@ -52,13 +52,25 @@ __device__ __forceinline__ Stat chan(Stat a, Stat b) {
 }
 
 // train-mode dropout after the SiLU (ResBlock.out_layers, unet.py:221)
+// `ctr` (optional, device memory): a step counter mixed into the seed when the kernel runs,
+// so a replayed HIP graph -- whose launch arguments, host seed included, are frozen at capture
+// -- draws a fresh mask each step (vd_set_dropout_counter).  Kernels call resolved() once.
 struct Drop {
   float p, inv_keep;
   uint64_t seed;
+  const uint64_t* ctr;
+  __device__ __forceinline__ Drop resolved() const {
+    Drop d = *this;
+    if (p > 0.f && ctr) d.seed = seed ^ ((*ctr + 1) * 0x9E3779B97F4A7C15ull);
+    d.ctr = nullptr;
+    return d;
+  }
   __device__ __forceinline__ float mul(int64_t idx) const {
     return p > 0.f ? dropout_mul(seed, idx, p, inv_keep) : 1.f;
   }
 };
+
+static const uint64_t* g_drop_ctr = nullptr;  // vd_set_dropout_counter
 
 // ---------------------------------------------------------------- forward
 // grid (nchunk, B).  Per WG: per-group (n, mean, M2) over its chunk.
@@ -164,7 +176,8 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict_
                                                             const float* __restrict__ rstd,
                                                             T* __restrict__ y, int64_t S, int C,
                                                             int G, int64_t chunk_px,
-                                                            int rows_per_iter, Drop drop) {
+                                                            int rows_per_iter, Drop drop_in) {
+  const Drop drop = drop_in.resolved();
   const int nvec = C / kVec, cpg = C / G;
   const int b = blockIdx.y, tid = threadIdx.x;
   const int r = tid / nvec, cv = tid % nvec;
@@ -199,7 +212,8 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
     int64_t S, int C, int G, int64_t chunk_px, int rows_per_iter, float* __restrict__ part,
-    Drop drop) {
+    Drop drop_in) {
+  const Drop drop = drop_in.resolved();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh = reinterpret_cast<float2*>(smem);  // [rows_per_iter][C]
   const int nvec = C / kVec;
@@ -324,7 +338,8 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ coef, T* __restrict__ dx, int64_t S, int C, int G, int64_t chunk_px,
-    int rows_per_iter, Drop drop) {
+    int rows_per_iter, Drop drop_in) {
+  const Drop drop = drop_in.resolved();
   const int nvec = C / kVec, cpg = C / G;
   const int b = blockIdx.y, tid = threadIdx.x;
   const int r = tid / nvec, cv = tid % nvec;
@@ -389,6 +404,8 @@ size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G) {
   return (fwd > bwd ? fwd : bwd) + 256;
 }
 
+void vd_set_dropout_counter(const uint64_t* counter) { g_drop_ctr = counter; }
+
 int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, void* y,
                           float* mean, float* rstd, int B, int64_t S, int C, int G, float eps,
                           int silu, float drop_p, uint64_t seed, int dtype, void* workspace,
@@ -398,7 +415,7 @@ int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, 
   VD_REQUIRE(gamma && beta && y && mean && rstd && workspace, "null argument");
   VD_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "dropout p=%f out of [0, 1)", drop_p);
   VD_REQUIRE(drop_p == 0.f || silu, "dropout is fused only after SiLU");
-  const Drop drop{drop_p, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, seed};
+  const Drop drop{drop_p, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, seed, g_drop_ctr};
   GNPlan p = gn_plan(B, S, C);
   float* part = reinterpret_cast<float*>(workspace);
   hipStream_t st = VD_STREAM(stream);
@@ -428,7 +445,7 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
   VD_REQUIRE(dy && gamma && beta && mean && rstd && dx && dgamma && dbeta && workspace,
              "null argument");
   VD_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "dropout p=%f out of [0, 1)", drop_p);
-  const Drop drop{drop_p, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, seed};
+  const Drop drop{drop_p, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, seed, g_drop_ctr};
   GNPlan p = gn_plan(B, S, C);
   float* part = reinterpret_cast<float*>(workspace);
   float* coef = part + (size_t)B * p.nchunk * C * 2;

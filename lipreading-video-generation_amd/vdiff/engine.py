@@ -69,12 +69,14 @@ class Trainer:
     train.py:102-103: Adam(model.parameters(), lr=1e-2), MSELoss."""
 
     def __init__(self, model, scheduler, lr=1e-2, bucket_mb=25.0, fused_adam=True,
-                 check_every=50, batch_pack=True):
+                 check_every=50, batch_pack=True, graph=False):
         """check_every: the loss finiteness flag (kept on the device, updated every step) is
         read on the host every `check_every` steps and by check_finite(); a non-finite
         loss raises FloatingPointError naming the first bad step.  0 disables it.
         batch_pack: re-pack the conv operands once per step in one launch
-        (ops.step_packed_weights) instead of per conv call."""
+        (ops.step_packed_weights) instead of per conv call.
+        graph: replay the denoiser's forward + backward as one HIP graph (TrainStepGraph);
+        one process only."""
         self.model = model
         self.scheduler = scheduler
         self.check_every = int(check_every)
@@ -89,8 +91,20 @@ class Trainer:
         self.opt = torch.optim.Adam(params, lr=lr, **kw)
         # conv operands re-packed once per step in one launch (ops.step_packed_weights)
         self.packs = ops.step_packed_weights() if batch_pack else contextlib.nullcontext()
+        if graph and self.bucketer is not None:
+            raise ValueError("Trainer(graph=True) is single-process (the gradient buckets are "
+                             "launched from autograd hooks)")
+        if graph and not batch_pack:
+            raise ValueError("Trainer(graph=True) needs batch_pack (per-call packs would be "
+                             "frozen into the graph)")
+        self.graph = TrainStepGraph(self) if graph else None
 
     def step(self, clip: Clip) -> torch.Tensor:
+        if self.graph is not None:
+            return self.graph.step(clip)
+        return self._eager_step(clip)
+
+    def _eager_step(self, clip: Clip) -> torch.Tensor:
         self.model.train()
         with self.packs:
             xt = self.scheduler.add_noise(clip.x0, clip.eps, clip.t)
@@ -129,6 +143,97 @@ class Trainer:
             if first >= 0:
                 raise FloatingPointError(f"non-finite training loss at step {first} "
                                          f"(of {self.steps_done})")
+
+
+class TrainStepGraph:
+    """Trainer.step with the denoiser replayed as one HIP graph (the
+    ~600 launch gaps of an eager step).
+
+    Captured: the batched weight pack, q_sample, the conditioning concat and the UNet forward,
+    the MSE and the whole backward down to the UNet parameters' gradients and the gradient of
+    the pooled audio features.  Eager around it: the wav2vec2 encoder (transformers draws its
+    LayerDrop and SpecAugment decisions on the host every step, which changes the launch
+    sequence, so it cannot be frozen), its backward (fed the replayed feature gradient) and
+    the fused Adam step over all parameters.  Same math as the eager step: the first `warmup`
+    steps run eagerly (lazy initialisation, the packed-weight plan), the capture itself does not
+    update anything, and the ResBlock dropout draws a new mask per replay through the device
+    counter the GroupNorm kernels read (vd_set_dropout_counter).  The UNet parameters' .grad
+    tensors live in the graph's memory pool and are overwritten by each replay; they are never
+    reset to None."""
+
+    def __init__(self, trainer, warmup=2):
+        self.tr = trainer
+        self.warmup = int(warmup)
+        self.g = None
+        self.steps = 0
+
+    def step(self, clip: Clip) -> torch.Tensor:
+        tr = self.tr
+        if self.steps < self.warmup:
+            self.steps += 1
+            return tr._eager_step(clip)
+        model = tr.model
+        model.train()
+        enc = model.encode_audio(clip.audio).float()
+        if self.g is None:
+            self._capture(clip, enc)
+        with torch.no_grad():
+            for dst, src in ((self.x0, clip.x0), (self.eps, clip.eps), (self.t, clip.t),
+                             (self.cond, clip.cond), (self.feats, enc)):
+                dst.copy_(src)
+        self.g.replay()
+        if enc.requires_grad:
+            enc.backward(self.feats.grad)
+        tr.opt.step()
+        for p in self.eager_params:
+            p.grad = None
+        self.steps += 1
+        loss = self.loss.clone()
+        tr._track_finite(loss)
+        return loss
+
+    def _body(self):
+        tr = self.tr
+        with tr.packs:
+            xt = tr.scheduler.add_noise(self.x0, self.eps, self.t)
+            pred = tr.model(xt, self.cond, self.feats, self.t)
+            loss = F.mse_loss(pred, self.eps)
+            loss.backward()
+        return loss.detach()
+
+    def _capture(self, clip, enc):
+        from . import _lib
+        tr, model = self.tr, self.tr.model
+        self.x0, self.eps = clip.x0.clone(), clip.eps.clone()
+        self.t, self.cond = clip.t.clone(), clip.cond.clone()
+        self.feats = enc.detach().clone().requires_grad_(enc.requires_grad)
+        enc_ids = {id(p) for p in model.audio_encoder.parameters()} \
+            if getattr(model, "audio_encoder", None) is not None else set()
+        self.eager_params = [p for p in model.parameters() if p.requires_grad and id(p) in enc_ids]
+        self.ctr = torch.zeros((), dtype=torch.int64, device=enc.device)
+        tr.opt.zero_grad(set_to_none=True)
+        # one run of the region on a side stream before capture (torch's graph recipe: lazy
+        # allocator / autograd state), its gradients discarded
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self._body()
+        torch.cuda.current_stream().wait_stream(side)
+        tr.opt.zero_grad(set_to_none=True)
+        self.feats.grad = None
+        self.g = torch.cuda.CUDAGraph()
+        lib = _lib.lib()
+        lib.vd_set_dropout_counter(self.ctr.data_ptr())
+        try:
+            with torch.cuda.graph(self.g, capture_error_mode="thread_local"):
+                self.ctr.add_(1)
+                self.loss = self._body()
+        finally:
+            lib.vd_set_dropout_counter(None)
+        missing = [n for n, p in model.named_parameters()
+                   if p.requires_grad and id(p) not in enc_ids and p.grad is None]
+        if missing:  # a parameter off the captured path would silently never train
+            raise RuntimeError(f"TrainStepGraph: no captured gradient for {missing[:4]}")
 
 
 @torch.no_grad()

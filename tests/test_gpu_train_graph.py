@@ -1,0 +1,139 @@
+"""Trainer(graph=True): the denoiser's forward + backward replayed as one HIP graph
+(vdiff.engine.TrainStepGraph) against the eager step, and the
+GroupNorm dropout step counter the replays advance (vd_set_dropout_counter)."""
+import copy
+
+import pytest
+import torch
+
+from oracle.fixtures import rel_l2
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+GOLDEN = 0x9E3779B97F4A7C15
+
+
+def _tiny_w2v(hidden=64):
+    """A one-layer wav2vec2 with every stochastic part off (dropouts, LayerDrop, SpecAugment),
+    so the eager and the graph runs see the same encoder computation."""
+    from transformers import Wav2Vec2Config, Wav2Vec2Model
+    from vdiff.unet_audio import Wav2Vec2Encoder, _patch_wav2vec2
+    cfg = Wav2Vec2Config(num_hidden_layers=1, hidden_size=hidden, intermediate_size=128,
+                         num_attention_heads=4, conv_dim=(64,) * 7, hidden_dropout=0.0,
+                         attention_dropout=0.0, activation_dropout=0.0, feat_proj_dropout=0.0,
+                         final_dropout=0.0, layerdrop=0.0, mask_time_prob=0.0,
+                         mask_feature_prob=0.0)
+    torch.manual_seed(11)
+    w = Wav2Vec2Model(cfg)
+    _patch_wav2vec2(w)
+    enc = Wav2Vec2Encoder.__new__(Wav2Vec2Encoder)
+    torch.nn.Module.__init__(enc)
+    enc.wav2vec2 = w
+    return enc
+
+
+def _model(dropout=0.0, audio=False, bf16=False):
+    from oracle.unet import init_params
+    from vdiff.unet_audio import UNetAudio
+    m = UNetAudio(image_size=32, in_channels=3, model_channels=32, out_channels=3,
+                  num_res_blocks=1, attention_resolutions=(2,), channel_mult=(1, 2), dims=3,
+                  audio_feature_dim=64, projected_audio_dim=16, im_cond_output_ch=16,
+                  dropout=dropout, audio_encoder=False)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    m.load_state_dict(init_params(shapes, 5))
+    if audio:
+        m.audio_encoder = _tiny_w2v()
+    if bf16:
+        m.convert_to_fp16()
+    return m.to(dev)
+
+
+def _clip(s, audio):
+    from vdiff.engine import Clip
+    gen = torch.Generator(device=dev).manual_seed(100 + s)
+    x0 = torch.rand((1, 3, 4, 32, 32), generator=gen, device=dev) * 2 - 1
+    cond = torch.rand((1, 3, 32, 32), generator=gen, device=dev) * 2 - 1
+    a = ({"input_values": torch.randn((4, 4000), generator=gen, device=dev)} if audio
+         else torch.randn((4, 64), generator=gen, device=dev))
+    eps = torch.randn(x0.shape, generator=gen, device=dev)
+    return Clip(x0, cond, a, eps, torch.tensor([3 + 7 * s], device=dev))
+
+
+def _run(m, graph, steps, audio, lr=1e-3):
+    from vdiff.engine import Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    tr = Trainer(m, LinearNoiseScheduler(100, 0.00085, 0.012), lr=lr, graph=graph)
+    losses = torch.stack([tr.step(_clip(s, audio)) for s in range(steps)])
+    return tr, losses
+
+
+@pytest.mark.parametrize("audio,bf16", [(False, False), (True, False), (False, True)])
+def test_graph_step_equals_eager(audio, bf16):
+    """Six steps (two eager warm-up steps, the capture, four replays) track the eager
+    Trainer: losses and every parameter after the last Adam step, fp32 1e-5 / bf16 1e-4
+    (the split-K weight-gradient atomics make any two runs differ in the last bits).
+    With a trainable (tiny, deterministic) wav2vec2 the encoder's backward is fed the
+    replayed feature gradient."""
+    m = _model(audio=audio, bf16=bf16)
+    me, mg = copy.deepcopy(m), copy.deepcopy(m)
+    _, le = _run(me, False, 6, audio)
+    tr, lg = _run(mg, True, 6, audio)
+    assert tr.graph.g is not None and tr.graph.steps == 6
+    tol = 1e-4 if bf16 else 1e-5
+    assert rel_l2(lg, le) < tol, (lg, le)
+    for (n, a), b in zip(me.named_parameters(), mg.parameters()):
+        assert rel_l2(b, a) < tol, n
+    if audio:  # the encoder trained in both runs
+        w0 = dict(m.named_parameters())
+        moved = [n for n, p in mg.named_parameters()
+                 if n.startswith("audio_encoder.") and not torch.equal(p, w0[n])]
+        assert len(moved) > 5
+
+
+def test_graph_replays_draw_new_dropout_masks():
+    """ResBlock dropout (0.1) in the graph: at lr 0 the same clip replayed twice gives two
+    different losses (a frozen seed would repeat the mask), while without dropout the two
+    replays agree."""
+    for dropout, differ in ((0.1, True), (0.0, False)):
+        from vdiff.engine import Trainer
+        from vdiff.schedulers import LinearNoiseScheduler
+        tr = Trainer(_model(dropout=dropout), LinearNoiseScheduler(100, 0.00085, 0.012), lr=0.0,
+                     graph=True)
+        c = _clip(0, False)
+        losses = [float(tr.step(c)) for _ in range(5)]
+        d = abs(losses[4] - losses[3])
+        if differ:
+            assert d > 1e-6 * abs(losses[3]), losses
+        else:
+            assert d < 1e-5 * abs(losses[3]), losses
+
+
+def test_dropout_counter_mixes_into_seed():
+    """vd_set_dropout_counter: a GroupNorm+SiLU+dropout launch that reads counter value k
+    equals the launch with seed ^ ((k + 1) * 0x9E3779B97F4A7C15) and no counter, forward and
+    backward."""
+    from vdiff import _lib, ops
+    lib = _lib.lib()
+    torch.manual_seed(3)
+    x = ops.to_cl(torch.randn(1, 64, 4, 8, 8, device=dev).bfloat16())
+    g = torch.randn(64, device=dev, requires_grad=True)
+    b = torch.randn(64, device=dev, requires_grad=True)
+    dy = torch.randn(x.shape, device=dev).bfloat16()
+
+    def run(seed, ctr=None):
+        xx = x.detach().clone().requires_grad_(True)
+        lib.vd_set_dropout_counter(ctr.data_ptr() if ctr is not None else None)
+        try:
+            y = ops.group_norm_silu(xx, g, b, 32, 1e-5, True, dropout=0.1, seed=seed)
+            dx, = torch.autograd.grad(y, xx, ops.to_cl(dy))
+        finally:
+            lib.vd_set_dropout_counter(None)
+        return y.detach(), dx
+
+    ctr = torch.full((), 5, dtype=torch.int64, device=dev)
+    y1, d1 = run(123, ctr)
+    y2, d2 = run(123 ^ ((6 * GOLDEN) % 2 ** 64))
+    y0, _ = run(123)
+    assert torch.equal(y1, y2) and torch.equal(d1, d2)
+    assert not torch.equal(y1, y0)
