@@ -177,6 +177,14 @@ class TrainStepGraph:
         enc = model.encode_audio(clip.audio).float()
         if self.g is None:
             self._capture(clip, enc)
+        elif self._shapes(clip, enc) != self.shapes:
+            # a batch of another shape (a short last batch): eager, with every gradient
+            # released first so that the eager backward does not accumulate into the graph's
+            tr.opt.zero_grad(set_to_none=True)
+            self.steps += 1
+            return tr._eager_step(clip)
+        for p, g in self.grads:  # (an eager step in between may have released them)
+            p.grad = g
         with torch.no_grad():
             for dst, src in ((self.x0, clip.x0), (self.eps, clip.eps), (self.t, clip.t),
                              (self.cond, clip.cond), (self.feats, enc)):
@@ -191,6 +199,10 @@ class TrainStepGraph:
         loss = self.loss.clone()
         tr._track_finite(loss)
         return loss
+
+    @staticmethod
+    def _shapes(clip, enc):
+        return tuple((tuple(x.shape), x.dtype) for x in (clip.x0, clip.eps, clip.t, clip.cond, enc))
 
     def _body(self):
         tr = self.tr
@@ -230,6 +242,8 @@ class TrainStepGraph:
                 self.loss = self._body()
         finally:
             lib.vd_set_dropout_counter(None)
+        self.shapes = self._shapes(clip, enc)
+        self.grads = [(p, p.grad) for p in model.parameters() if p.grad is not None]
         missing = [n for n, p in model.named_parameters()
                    if p.requires_grad and id(p) not in enc_ids and p.grad is None]
         if missing:  # a parameter off the captured path would silently never train

@@ -49,13 +49,13 @@ def _model(dropout=0.0, audio=False, bf16=False):
     return m.to(dev)
 
 
-def _clip(s, audio):
+def _clip(s, audio, frames=4):
     from vdiff.engine import Clip
     gen = torch.Generator(device=dev).manual_seed(100 + s)
-    x0 = torch.rand((1, 3, 4, 32, 32), generator=gen, device=dev) * 2 - 1
+    x0 = torch.rand((1, 3, frames, 32, 32), generator=gen, device=dev) * 2 - 1
     cond = torch.rand((1, 3, 32, 32), generator=gen, device=dev) * 2 - 1
-    a = ({"input_values": torch.randn((4, 4000), generator=gen, device=dev)} if audio
-         else torch.randn((4, 64), generator=gen, device=dev))
+    a = ({"input_values": torch.randn((frames, 4000), generator=gen, device=dev)} if audio
+         else torch.randn((frames, 64), generator=gen, device=dev))
     eps = torch.randn(x0.shape, generator=gen, device=dev)
     return Clip(x0, cond, a, eps, torch.tensor([3 + 7 * s], device=dev))
 
@@ -89,6 +89,25 @@ def test_graph_step_equals_eager(audio, bf16):
         moved = [n for n, p in mg.named_parameters()
                  if n.startswith("audio_encoder.") and not torch.equal(p, w0[n])]
         assert len(moved) > 5
+
+
+def test_graph_step_other_shape_runs_eager():
+    """A batch of another shape after the capture (a short last batch) runs eagerly and the
+    replays after it still train every parameter: the sequence 4-frame x4, 2-frame, 4-frame x2
+    tracks the eager Trainer (fp32, 1e-5)."""
+    from vdiff.engine import Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    m = _model()
+    seq = [(0, 4), (1, 4), (2, 4), (3, 4), (4, 2), (5, 4), (6, 4)]
+    out = []
+    for graph in (False, True):
+        mm = copy.deepcopy(m)
+        tr = Trainer(mm, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-3, graph=graph)
+        losses = torch.stack([tr.step(_clip(s, False, f)) for s, f in seq])
+        out.append((losses, [p.detach().clone() for p in mm.parameters()]))
+    assert rel_l2(out[1][0], out[0][0]) < 1e-5
+    for a, b in zip(out[0][1], out[1][1]):
+        assert rel_l2(b, a) < 1e-5
 
 
 def test_graph_replays_draw_new_dropout_masks():
