@@ -393,34 +393,47 @@ def xattn_leg(args, rank, world, device, base_ms):
     return out
 
 
-def graph_leg(args, device, base_ms):
-    """Auxiliary (one process): the same train step with the denoiser's forward + backward
-    replayed as one HIP graph (Trainer(graph=True), vdiff.engine.TrainStepGraph; wav2vec2 and
-    Adam eager around it), from a fresh model of the same init: max(3, warmup) untimed steps
-    (two eager, the capture), then --steps timed replays.  The headline `value` stays the
-    eager step, whose per-launch attention events the roofline needs."""
+def graph_leg(args, device):
+    """Auxiliary (one process): the train step with the denoiser's forward + backward replayed
+    as one HIP graph (Trainer(graph=True), vdiff.engine.TrainStepGraph; wav2vec2 and Adam
+    eager around it) against the eager step, PAIRED: two models from the same init, one per
+    mode, stepped alternately on the same clip, so both see the same weights (the attention
+    kernels' clock follows the operands) and the same box state.  max(3,
+    warmup) untimed steps each (graph: two eager, the capture), then --steps timed steps each;
+    per-step times are medians.  The headline `value` stays the eager step of the main leg,
+    whose per-launch attention events the roofline needs."""
+    import statistics
     from vdiff.engine import Trainer, synthetic_clip
     from vdiff.schedulers import LinearNoiseScheduler
-    torch.manual_seed(1234)
-    model = build_model(args, device)
-    tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2, graph=True)
+    trainers = {}
+    for mode in ("eager", "graph"):
+        torch.manual_seed(1234)
+        model = build_model(args, device)
+        trainers[mode] = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2,
+                                 graph=mode == "graph")
     clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=0)
     for _ in range(max(3, args.warmup)):
-        tr.step(clip)
+        for tr in trainers.values():
+            tr.step(clip)
+    times = {m: [] for m in trainers}
+    losses = {}
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = tr.step(clip)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    ms = el / args.steps * 1e3
-    out = {"metric": "train-step frames/sec, denoiser fwd+bwd as one HIP graph",
-           "value": round(args.clips_per_gpu * args.frames * args.steps / el, 4),
-           "unit": "frames/s", "ms_per_step": round(ms, 2),
-           "ms_vs_eager": round(ms - base_ms, 2) if base_ms else None,
-           "loss": round(float(loss), 4)}
-    log(f"train graph: {ms:.1f} ms/step")
-    del tr, model
+        for m, tr in trainers.items():
+            t0 = time.perf_counter()
+            losses[m] = tr.step(clip)
+            torch.cuda.synchronize()
+            times[m].append((time.perf_counter() - t0) * 1e3)
+    med = {m: statistics.median(v) for m, v in times.items()}
+    out = {"metric": "train-step ms, denoiser fwd+bwd as one HIP graph vs eager (paired)",
+           "ms_per_step_graph": round(med["graph"], 2), "ms_per_step_eager": round(med["eager"], 2),
+           "ms_saved": round(med["eager"] - med["graph"], 2),
+           "value": round(args.clips_per_gpu * args.frames / (med["graph"] / 1e3), 4),
+           "unit": "frames/s", "steps_timed": args.steps,
+           "loss_graph": round(float(losses["graph"]), 4),
+           "loss_eager": round(float(losses["eager"]), 4)}
+    log(f"train graph vs eager (paired): {med['graph']:.1f} vs {med['eager']:.1f} ms/step")
+    del trainers
     torch.cuda.empty_cache()
     return out
 
@@ -625,7 +638,7 @@ def main():
 
     if args.only in ("train", "all") and args.train_graph and world == 1:
         try:  # an auxiliary leg: never let it take the headline numbers down
-            result["train_graph"] = graph_leg(args, device, result.get("ms_per_step"))
+            result["train_graph"] = graph_leg(args, device)
         except Exception as e:
             log(f"train graph leg failed: {type(e).__name__}: {e}")
             result["train_graph"] = {"value": None, "error": f"{type(e).__name__}: {e}"}

@@ -297,23 +297,28 @@ __global__ __launch_bounds__(256) void channel_sums_kernel(const T* __restrict__
   }
 }
 
-// 32 channels per block, 8 row lanes per channel (independent loads in flight), LDS reduce
-__global__ __launch_bounds__(256) void channel_sums_finish_kernel(const float* __restrict__ part,
-                                                                  int nblk, int C,
-                                                                  float* __restrict__ out) {
-  __shared__ float red[8][33];
+// 32 channels per block, 32 row lanes per channel: at most 8 independent partial loads per
+// lane (kSumBlocks = 256), all in flight before the adds; fixed-order LDS reduce
+__global__ __launch_bounds__(1024) void channel_sums_finish_kernel(const float* __restrict__ part,
+                                                                   int nblk, int C,
+                                                                   float* __restrict__ out) {
+  __shared__ float red[32][33];
   const int cl = threadIdx.x & 31, kl = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl, b = blockIdx.y;
-  float sum = 0.f;
-  if (c < C) {
-    const float* p = part + (int64_t)b * nblk * C + c;
-    for (int k = kl; k < nblk; k += 8) sum += p[(int64_t)k * C];
+  float v[kSumBlocks / 32];
+#pragma unroll
+  for (int i = 0; i < kSumBlocks / 32; ++i) {
+    const int k = kl + 32 * i;
+    v[i] = (c < C && k < nblk) ? part[((int64_t)b * nblk + k) * C + c] : 0.f;
   }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < kSumBlocks / 32; ++i) sum += v[i];
   red[kl][cl] = sum;
   __syncthreads();
   if (kl == 0 && c < C) {
 #pragma unroll
-    for (int k = 1; k < 8; ++k) sum += red[k][cl];
+    for (int k = 1; k < 32; ++k) sum += red[k][cl];
     out[(int64_t)b * C + c] = sum;
   }
 }
@@ -508,7 +513,7 @@ int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dty
   return VD_DISPATCH_DTYPE(dtype, Tp, {
     channel_sums_kernel<Tp><<<dim3((unsigned)blocks, (unsigned)B), 256, 0, st>>>(
         (const Tp*)x, S, C, cs, rows, part);
-    channel_sums_finish_kernel<<<dim3((unsigned)vd_cdiv(C, 32), (unsigned)B), 256, 0, st>>>(
+    channel_sums_finish_kernel<<<dim3((unsigned)vd_cdiv(C, 32), (unsigned)B), 1024, 0, st>>>(
         part, (int)blocks, C, out);
   });
 }

@@ -212,8 +212,12 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
     int64_t S, int C, int G, int64_t chunk_px, int rows_per_iter, float* __restrict__ part,
-    Drop drop_in) {
+    Drop drop_in, float* __restrict__ zero, int nzero) {
   const Drop drop = drop_in.resolved();
+  // the first workgroup clears gn_bwd_sum_kernel's atomic targets (it runs after this kernel
+  // in stream order): no separate memset launch
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0.f;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh = reinterpret_cast<float2*>(smem);  // [rows_per_iter][C]
   const int nvec = C / kVec;
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(1024) void gn_bwd_sum_kernel(const float* __restric
                                                           int nchunk, int C, int kper,
                                                           float* __restrict__ sums) {
   // grid (C / 64, B, splits): this WG sums chunks [z * kper, (z + 1) * kper) and adds into
-  // sums (zeroed by the launcher) -- enough workgroups to stream the partials at speed
+  // sums (zeroed by gn_bwd_reduce_kernel) -- enough workgroups to stream the partials at speed
   __shared__ float2 sh[16][64];
   const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
@@ -457,12 +461,11 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
     if (silu)
       gn_bwd_reduce_kernel<T, true><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part, drop);
+          p.rows_per_iter, part, drop, sums, B * C * 2);
     else
       gn_bwd_reduce_kernel<T, false><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part, drop);
-    (void)hipMemsetAsync(sums, 0, (size_t)B * C * 2 * sizeof(float), st);
+          p.rows_per_iter, part, drop, sums, B * C * 2);
     const int kper = 64, ksplit = (int)vd_cdiv(p.nchunk, kper);
     gn_bwd_sum_kernel<<<dim3((unsigned)vd_cdiv(C, 64), B, ksplit), 1024, 0, st>>>(
         part, p.nchunk, C, kper, sums);
