@@ -83,8 +83,9 @@ def parse():
     ap.add_argument("--xattn-steps", type=int, default=3,
                     help="timed train steps with audio cross-attention (build extension, "
                          "auxiliary leg); 0 skips it")
-    ap.add_argument("--no-train-graph", dest="train_graph", action="store_false",
-                    help="skip the auxiliary graph-replayed train-step leg")
+    ap.add_argument("--train-graph", action="store_true",
+                    help="auxiliary leg: graph-replayed train step paired with an eager one "
+                         "(DESIGN section 9 item 3)")
     ap.add_argument("--timer-convs", action="store_true",
                     help="per-launch conv events inside the timed train steps too (the round-2 "
                          "measurement; A/B of the events' own cost)")
@@ -345,7 +346,7 @@ def vivit_leg(args, rank, world, device):
            "heads": cfg.num_attention_heads, "train_tflop_per_step": round(flop / 1e12, 4),
            "model_tflops_per_gpu": round(flop / (el / args.vivit_steps) / 1e12, 2),
            "bound": "launch (9 tokens x 256 hidden: microsecond kernels)",
-           "parallelism": f"dp{world}", "loss": round(float(loss), 4),
+           "parallelism": f"dp{world}", "loss": _num(loss),
            "hip_graph": graph}
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
@@ -386,11 +387,17 @@ def xattn_leg(args, rank, world, device, base_ms):
            "unit": "frames/s", "ms_per_step": round(ms, 2),
            "overhead_ms_vs_concat_only": round(ms - base_ms, 2) if base_ms else None,
            "fwd_tflop_per_clip": round(work.total / 1e12, 3), "audio_tokens_per_frame": 12,
-           "loss": round(float(loss), 4)}
+           "loss": _num(loss)}
     log(f"xattn: {ms:.1f} ms/step")
     del tr, model
     torch.cuda.empty_cache()
     return out
+
+
+def _num(x, nd=4):
+    """A float for the JSON line: None when not finite (NaN / Infinity are not JSON)."""
+    x = float(x)
+    return round(x, nd) if math.isfinite(x) else None
 
 
 def graph_leg(args, device):
@@ -409,19 +416,21 @@ def graph_leg(args, device):
     for mode in ("eager", "graph"):
         torch.manual_seed(1234)
         model = build_model(args, device)
+        # VDIFF_GRAPH_LEG_EAGER=1: both trainers eager (the run-to-run spread of the losses)
+        graph = mode == "graph" and not os.environ.get("VDIFF_GRAPH_LEG_EAGER")
         trainers[mode] = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2,
-                                 graph=mode == "graph")
+                                 graph=graph)
     clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=0)
+    seq = {m: [] for m in trainers}
     for _ in range(max(3, args.warmup)):
-        for tr in trainers.values():
-            tr.step(clip)
+        for m, tr in trainers.items():
+            seq[m].append(tr.step(clip))
     times = {m: [] for m in trainers}
-    losses = {}
     torch.cuda.synchronize()
     for _ in range(args.steps):
         for m, tr in trainers.items():
             t0 = time.perf_counter()
-            losses[m] = tr.step(clip)
+            seq[m].append(tr.step(clip))
             torch.cuda.synchronize()
             times[m].append((time.perf_counter() - t0) * 1e3)
     med = {m: statistics.median(v) for m, v in times.items()}
@@ -430,8 +439,8 @@ def graph_leg(args, device):
            "ms_saved": round(med["eager"] - med["graph"], 2),
            "value": round(args.clips_per_gpu * args.frames / (med["graph"] / 1e3), 4),
            "unit": "frames/s", "steps_timed": args.steps,
-           "loss_graph": round(float(losses["graph"]), 4),
-           "loss_eager": round(float(losses["eager"]), 4)}
+           "losses_graph": [_num(x) for x in seq["graph"]],
+           "losses_eager": [_num(x) for x in seq["eager"]]}
     log(f"train graph vs eager (paired): {med['graph']:.1f} vs {med['eager']:.1f} ms/step")
     del trainers
     torch.cuda.empty_cache()

@@ -331,8 +331,11 @@ def test_trainer_batched_pack_equals_per_call_pack():
     """the conv operands re-packed once per step in one launch
     (ops.step_packed_weights, vd_conv_pack_weights) are bit-identical to per-call packs of
     the same weights, from the second step on no per-call pack runs for a Parameter, and
-    three bf16 train steps track the per-call run (the split-K weight-gradient atomics make
-    runs differ in the last fp32 bits, so parameters are compared at 1e-5)."""
+    three bf16 train steps track the per-call run.  The split-K weight-gradient and GroupNorm
+    atomics make any two runs differ in the last fp32 bits, and Adam's g / (|g| + eps) turns
+    that into +-lr steps where a gradient is zero in exact arithmetic, so the losses are held
+    to 1e-4 (measured 0 - 2.1e-5 between runs) and every parameter to 1e-5 or four times the
+    per-call run's own repeat."""
     import copy
     from vdiff import ops
     from vdiff.engine import Clip, Trainer
@@ -347,7 +350,7 @@ def test_trainer_batched_pack_equals_per_call_pack():
     m.convert_to_fp16()
     m = m.to(dev)
     runs = []
-    for batch_pack in (False, True):
+    for batch_pack in (False, False, True):
         mm = copy.deepcopy(m)
         tr = Trainer(mm, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-3,
                      batch_pack=batch_pack)
@@ -375,9 +378,10 @@ def test_trainer_batched_pack_equals_per_call_pack():
     with sp:
         for k, (w, Co, Ci, taps, Cip, Cop, trn, dt) in sp.want.items():
             assert torch.equal(sp.bufs[k], ops._pack_weight_now(w, Co, Ci, taps, Cip, Cop, trn, dt))
-    assert rel_l2(runs[1][0], runs[0][0]) < 1e-5
-    for a, b in zip(runs[0][1], runs[1][1]):
-        assert rel_l2(b, a) < 1e-5
+    assert rel_l2(runs[2][0], runs[0][0]) < 1e-4
+    for a, a2, b in zip(runs[0][1], runs[1][1], runs[2][1]):
+        d = rel_l2(b, a)
+        assert d < 1e-5 or d < 4 * rel_l2(a2, a) + 1e-5, d
 
 
 def test_batched_pack_plan_survives_moved_weights():
