@@ -235,11 +235,13 @@ class TrainStepGraph:
         self.feats.grad = None
         self.g = torch.cuda.CUDAGraph()
         lib = _lib.lib()
+        # the graph's loss output goes to a buffer allocated outside its memory pool
+        self.loss = torch.zeros((), dtype=torch.float32, device=enc.device)
         lib.vd_set_dropout_counter(self.ctr.data_ptr())
         try:
             with torch.cuda.graph(self.g, capture_error_mode="thread_local"):
                 self.ctr.add_(1)
-                self.loss = self._body()
+                self.loss.copy_(self._body())
         finally:
             lib.vd_set_dropout_counter(None)
         self.shapes = self._shapes(clip, enc)
