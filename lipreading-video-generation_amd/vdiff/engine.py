@@ -13,6 +13,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+import warnings
 from dataclasses import dataclass
 
 import torch
@@ -97,6 +98,11 @@ class Trainer:
         if graph and not batch_pack:
             raise ValueError("Trainer(graph=True) needs batch_pack (per-call packs would be "
                              "frozen into the graph)")
+        if graph:
+            warnings.warn("Trainer(graph=True) is experimental: at the config-2 scale (bf16, "
+                          "dropout 0.1, wav2vec2-base, lr 1e-2) replays returned negative / "
+                          "non-finite losses (DESIGN section 9 item 3); small models match the "
+                          "eager step")
         self.graph = TrainStepGraph(self) if graph else None
 
     def step(self, clip: Clip) -> torch.Tensor:

@@ -61,9 +61,6 @@ def parse(argv=None):
     ap.add_argument("--audio-attention", action="store_true",
                     help="audio cross-attention branches in every attention block (build "
                          "extension; the reference conditions by concatenation only)")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the denoiser's forward + backward as one HIP graph (one process; "
-                         "vdiff.engine.TrainStepGraph)")
     ap.add_argument("--ckpt", default="best_diffusion.pth")
     ap.add_argument("--resume", default=None, help="checkpoint with model/optimizer/step")
     ap.add_argument("--seed", type=int, default=0)
@@ -105,7 +102,7 @@ def train(argv=None):
         reinit_nonzero(model, seed=args.seed)
     model = model.to(device)
     broadcast_parameters(model)
-    trainer = Trainer(model, scheduler, lr=args.lr, graph=args.graph and world == 1)
+    trainer = Trainer(model, scheduler, lr=args.lr)
     start_epoch = 0
     if args.resume:
         state = torch.load(args.resume, map_location=device, weights_only=True)
