@@ -109,7 +109,8 @@ def build_model(args, device, audio_attention=False):
                           num_res_blocks=2, attention_resolutions=(1, 2, 4),
                           audio_feature_dim=768, projected_audio_dim=128, dims=3,
                           use_bf16=args.dtype == "bf16", attention_mode=args.mode,
-                          audio_encoder_pretrained=False, audio_attention=audio_attention)
+                          audio_encoder_pretrained=False, audio_attention=audio_attention,
+                          dropout=float(os.environ.get("VDIFF_BENCH_DROPOUT", "0.1")))
     reinit_nonzero(model, seed=1234)
     return model.to(device)
 
