@@ -91,6 +91,10 @@ def parse():
                          "measurement; A/B of the events' own cost)")
     ap.add_argument("--c4-steps", type=int, default=3,
                     help="timed DDIM steps at BASELINE config 4 (256x256x25); 0 skips the leg")
+    ap.add_argument("--lr", type=float, default=1e-2, help="Adam lr (train.py:102: 1e-2)")
+    ap.add_argument("--init", choices=["nonzero", "reference"], default="nonzero",
+                    help="train-leg init: 'nonzero' re-initialises the reference's zero_module "
+                         "layers (engine.reinit_nonzero); 'reference' keeps train.py's init")
     return ap.parse_args()
 
 
@@ -99,7 +103,7 @@ def log(*a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def build_model(args, device, audio_attention=False):
+def build_model(args, device, audio_attention=False, init=None):
     from vdiff.engine import reinit_nonzero
     from vdiff.unet_audio import UNetAudio
     import warnings
@@ -111,7 +115,8 @@ def build_model(args, device, audio_attention=False):
                           use_bf16=args.dtype == "bf16", attention_mode=args.mode,
                           audio_encoder_pretrained=False, audio_attention=audio_attention,
                           dropout=float(os.environ.get("VDIFF_BENCH_DROPOUT", "0.1")))
-    reinit_nonzero(model, seed=1234)
+    if (init or getattr(args, "init", "nonzero")) == "nonzero":
+        reinit_nonzero(model, seed=1234)
     return model.to(device)
 
 
@@ -509,6 +514,12 @@ def main():
 
     model = build_model(args, device)
     broadcast_parameters(model)
+    # the DDIM / config-4 legs time the benchmark init (reinit_nonzero), not the weights the
+    # train leg's Adam steps leave behind
+    if args.init == "nonzero":
+        init_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    else:
+        init_state = build_model(args, device, init="nonzero").state_dict()
     nparams = sum(p.numel() for p in model.parameters())
     in_shape = (args.clips_per_gpu, 195, args.frames, args.size, args.size)
     work = unet_forward_work(model, in_shape)
@@ -524,11 +535,13 @@ def main():
 
     sched = LinearNoiseScheduler(100, 0.00085, 0.012)  # train.py:48-52
     rows = []
+    train_losses = []
     if args.only in ("train", "all"):
-        trainer = Trainer(model, sched, lr=1e-2)
+        trainer = Trainer(model, sched, lr=args.lr)
         clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
         for i in range(args.warmup):
             loss = trainer.step(clip)
+            train_losses.append(loss)
             log(f"warmup {i}: loss {float(loss):.4f}")
         barrier_sync(world)
         # attention launches only: the roofline's per-launch times (the conv breakdown comes
@@ -540,6 +553,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(args.steps):
             loss = trainer.step(clip)
+            train_losses.append(loss)  # device scalars: read after the timed region
         barrier_sync(world)
         el = time.perf_counter() - t0
         ops.set_timer(None)
@@ -557,6 +571,10 @@ def main():
         result["attention_units"] = units
         step_flops = 3 * work.total * args.clips_per_gpu
         result["model_tflops_per_gpu"] = round(step_flops / (el / args.steps) / 1e12, 1)
+        # rank 0's MSE losses, warm-up then timed steps (train.py:131-132 prints them)
+        result["train_losses"] = [_num(x, 5) for x in train_losses]
+        result["train_init"] = {"init": args.init, "lr": args.lr,
+                                "warmup_steps": args.warmup, "timed_steps": args.steps}
         log(f"train: {ms:.1f} ms/step, {result['value']:.3f} frames/s, loss {float(loss):.4f}, "
             f"model {result['model_tflops_per_gpu']} TFLOP/s/GPU (3x fwd)")
         for r in rows:
@@ -584,6 +602,8 @@ def main():
         torch.cuda.empty_cache()
 
     if args.only in ("ddim", "all"):
+        with torch.no_grad():
+            model.load_state_dict(init_state)
         kd = args.ddim_steps or args.steps
         sampler = DDIMSampler(LinearNoiseSchedulerV2(500, 0.00005, 0.015), steps=50)
         clip = synthetic_clip(1, args.frames, args.size, 500, device, seed=100 + rank)
@@ -676,10 +696,14 @@ def main():
             result["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
     else:
         result["cpu_baseline"] = None
+    bad = [i for i, x in enumerate(result.get("train_losses", [])) if x is None]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if bad:  # a diverged step: the line is printed (with the losses) but the run fails
+        log(f"error: non-finite training loss at steps {bad}")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -149,13 +149,17 @@ int vd_silu_bwd(const void* x, const void* dy, void* dx, int64_t n, int dtype,
  * with (ys, xs) the torch "nearest" source of (y, x) for an (h, w) -> (H, W)
  * resize (the 1x1 cond conv commutes with it and runs at (h, w)).  imc is
  * broadcast over T (one reference image per clip) and audio over (H, W).
- * bwd: d_imc[b][h][w][Ci] and d_audio[b][T][Ca] (fp32) are OVERWRITTEN. */
+ * bwd: d_imc[b][h][w][Ci] and d_audio[b][T][Ca] (fp32) are OVERWRITTEN, with fixed-order
+ * sums (bit-reproducible; d_audio through a caller workspace of
+ * vd_cond_concat_bwd_workspace_size bytes). */
 int vd_cond_concat(const void* image, const void* imc, const void* audio,
                    void* out, int B, int T, int H, int W, int Cx, int h, int w,
                    int Ci, int Ca, int out_cstride, int dtype, void* stream);
+size_t vd_cond_concat_bwd_workspace_size(int B, int T, int H, int W, int Ca);
 int vd_cond_concat_bwd(const void* dout, float* d_imc, float* d_audio, int B,
                        int T, int H, int W, int Cx, int h, int w, int Ci,
-                       int Ca, int out_cstride, int dtype, void* stream);
+                       int Ca, int out_cstride, int dtype, void* workspace,
+                       void* stream);
 
 /* ---- Upsample (nearest, x2 on H and W) --------------------------------
  * replaces unet.py:112-122 F.interpolate(..., mode="nearest") with the
@@ -198,6 +202,17 @@ int vd_conv3d_bwd_data(const vd_conv_desc* d, const void* dy,
 /* dw[Co][taps][Ci] += sum over output pixels of dy (x) x  (fp32) */
 int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy,
                          float* dw, void* stream);
+/* Deterministic weight gradient (the default of the Python ops since round 4): every pixel
+ * split writes its fp32 partial dW into its own slice of `workspace`
+ * (vd_conv3d_bwd_weight_workspace_size bytes), then one pass adds the slices in a fixed
+ * order and WRITES dw in the torch layout [Co_out][Ci_out][taps] (Co_out <= d->Co and
+ * Ci_out <= d->Ci drop the channel padding).  Bit-reproducible run to run; no zero fill
+ * and no layout permute are needed.  Replaces the weight half of conv_nd's autograd
+ * (utils.py:59-69) as vd_conv3d_bwd_weight does. */
+size_t vd_conv3d_bwd_weight_workspace_size(const vd_conv_desc* d);
+int vd_conv3d_bwd_weight_det(const vd_conv_desc* d, const void* x, const void* dy, float* dw,
+                             int Co_out, int Ci_out, void* workspace, size_t workspace_bytes,
+                             void* stream);
 
 /* Which 3x3x3 stride-1 bf16 convs (fwd / bwd-data) take the halo-tile kernel: 0 none, 1 every
  * eligible shape (W % 16 == 0, pad 1), 2 (default) the shapes where it measured faster

@@ -103,10 +103,10 @@ __global__ void cond_concat_vec_kernel(const T* __restrict__ image, const T* __r
   }
 }
 
-// d_audio[b][t][c] = sum over (y, x); grid (B*T, chunks of rows), atomics across chunks
+// d_audio partials: part[chunk][bt][c] = sum over the chunk's (y, x) rows; grid (B*T, chunks)
 template <typename T>
-__global__ void cond_audio_bwd_kernel(const T* __restrict__ dout, float* __restrict__ da, int H,
-                                      int W, int off, int Ca, int Cs, int rows_per_block) {
+__global__ void cond_audio_bwd_kernel(const T* __restrict__ dout, float* __restrict__ part, int BT,
+                                      int H, int W, int off, int Ca, int Cs, int rows_per_block) {
   const int bt = blockIdx.x;
   const int64_t HW = (int64_t)H * W;
   const int64_t p0 = (int64_t)blockIdx.y * rows_per_block;
@@ -116,30 +116,55 @@ __global__ void cond_audio_bwd_kernel(const T* __restrict__ dout, float* __restr
     float s = 0.f;
     for (int64_t p = p0; p < p1; ++p)
       s += Elem<T>::ld(dout + ((int64_t)bt * HW + p) * Cs + off + c);
-    atomicAdd(da + (int64_t)bt * Ca + c, s);
+    part[((int64_t)blockIdx.y * BT + bt) * Ca + c] = s;
   }
 }
 
-// d_imc[b][ys][xs][c] += sum over t and the (y, x) whose nearest source is (ys, xs)
+// d_audio[bt][c] = the chunk partials added in ascending chunk order (bit-reproducible; the
+// round-3 kernel added them with float atomics in arrival order)
+__global__ void cond_audio_finish_kernel(const float* __restrict__ part, int chunks, int64_t n,
+                                         float* __restrict__ da) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < chunks; ++k) s += part[k * n + i];
+  da[i] = s;
+}
+
+// first destination index whose nearest source is >= src (nearest_src is non-decreasing)
+__device__ __forceinline__ int nearest_first(int src, int in, int out) {
+  int d = (int)(((int64_t)src * out) / in) - 2;
+  if (d < 0) d = 0;
+  while (d < out && nearest_src(d, in, out) < src) ++d;
+  return d;
+}
+
+// d_imc[b][ys][xs][c] = sum over t and the (y, x) whose nearest source is (ys, xs): each
+// thread owns one source element and walks its preimage rectangle in a fixed order
+// (no atomics: bit-reproducible for any resize ratio)
 template <typename T>
 __global__ void cond_imc_bwd_kernel(const T* __restrict__ dout, float* __restrict__ di, int B,
                                     int T_, int H, int W, int off, int h, int w, int Ci, int Cs) {
-  const int64_t n = (int64_t)B * H * W * Ci;
+  const int64_t n = (int64_t)B * h * w * Ci;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % Ci);
-    int64_t p = i / Ci;
-    const int x = (int)(p % W);
-    p /= W;
-    const int y = (int)(p % H);
-    const int b = (int)(p / H);
+    int64_t q = i / Ci;
+    const int xs = (int)(q % w);
+    q /= w;
+    const int ys = (int)(q % h);
+    const int b = (int)(q / h);
+    const int y0 = nearest_first(ys, h, H), x0 = nearest_first(xs, w, W);
     float s = 0.f;
     for (int t = 0; t < T_; ++t)
-      s += Elem<T>::ld(dout + ((((int64_t)b * T_ + t) * H + y) * W + x) * Cs + off + c);
-    const int ys = nearest_src(y, h, H), xs = nearest_src(x, w, W);
-    atomicAdd(di + (((int64_t)b * h + ys) * w + xs) * Ci + c, s);
+      for (int y = y0; y < H && nearest_src(y, h, H) == ys; ++y)
+        for (int x = x0; x < W && nearest_src(x, w, W) == xs; ++x)
+          s += Elem<T>::ld(dout + ((((int64_t)b * T_ + t) * H + y) * W + x) * Cs + off + c);
+    di[i] = s;
   }
 }
+
+constexpr int kAudioRows = 256;  // (y, x) rows per d_audio partial
 
 }  // namespace
 
@@ -186,25 +211,31 @@ int vd_cond_concat(const void* image, const void* imc, const void* audio, void* 
   });
 }
 
+size_t vd_cond_concat_bwd_workspace_size(int B, int T, int H, int W, int Ca) {
+  if (B <= 0 || T <= 0 || H <= 0 || W <= 0 || Ca <= 0) return 0;
+  return (size_t)vd_cdiv((int64_t)H * W, kAudioRows) * B * T * Ca * sizeof(float) + 256;
+}
+
 int vd_cond_concat_bwd(const void* dout, float* d_imc, float* d_audio, int B, int T, int H, int W,
                        int Cx, int h, int w, int Ci, int Ca, int out_cstride, int dtype,
-                       void* stream) {
+                       void* workspace, void* stream) {
   VD_REQUIRE(dout, "null tensor");
   VD_REQUIRE(B > 0 && T > 0 && H > 0 && W > 0 && h > 0 && w > 0, "bad shape");
+  VD_REQUIRE(!(d_audio && Ca > 0) || workspace, "d_audio needs the workspace");
   hipStream_t st = VD_STREAM(stream);
-  if (d_imc && Ci > 0 && hipMemsetAsync(d_imc, 0, sizeof(float) * B * h * w * Ci, st))
-    return vd::fail(VD_ELAUNCH, "memset d_imc");
-  if (d_audio && Ca > 0 && hipMemsetAsync(d_audio, 0, sizeof(float) * B * T * Ca, st))
-    return vd::fail(VD_ELAUNCH, "memset d_audio");
   return VD_DISPATCH_DTYPE(dtype, Tp, {
     if (d_audio && Ca > 0) {
-      const int rows = 256;
-      dim3 grid((unsigned)(B * T), (unsigned)vd_cdiv((int64_t)H * W, rows));
-      cond_audio_bwd_kernel<Tp><<<grid, 128, 0, st>>>((const Tp*)dout, d_audio, H, W, Cx + Ci, Ca,
-                                                      out_cstride, rows);
+      const int chunks = (int)vd_cdiv((int64_t)H * W, kAudioRows);
+      float* part = reinterpret_cast<float*>(workspace);
+      dim3 grid((unsigned)(B * T), (unsigned)chunks);
+      cond_audio_bwd_kernel<Tp><<<grid, 128, 0, st>>>((const Tp*)dout, part, B * T, H, W,
+                                                      Cx + Ci, Ca, out_cstride, kAudioRows);
+      const int64_t n = (int64_t)B * T * Ca;
+      cond_audio_finish_kernel<<<(unsigned)vd_cdiv(n, 256), 256, 0, st>>>(part, chunks, n,
+                                                                          d_audio);
     }
     if (d_imc && Ci > 0) {
-      const int64_t n = (int64_t)B * H * W * Ci;
+      const int64_t n = (int64_t)B * h * w * Ci;
       cond_imc_bwd_kernel<Tp><<<grid_for(n), kBlock, 0, st>>>((const Tp*)dout, d_imc, B, T, H, W,
                                                               Cx, h, w, Ci, out_cstride);
     }

@@ -265,7 +265,18 @@ struct WgtGeom {
   int kt, kh, kw, st, sh, sw, pt, ph, pw;
   int64_t M;                // B*To*Ho*Wo
   int64_t m_per_split;
+  // 0: atomicAdd into dw (vd_conv3d_bwd_weight).  > 0: split y WRITES its partial dW to
+  // dw + y * split_stride (vd_conv3d_bwd_weight_det; summed in a fixed order afterwards)
+  int64_t split_stride;
 };
+
+// one fp32 partial of dW: accumulated (atomics) or stored into the split's own slice
+__device__ __forceinline__ void wg_out(const WgtGeom& g, float* dw, int64_t off, float v) {
+  if (g.split_stride)
+    dw[(int64_t)blockIdx.y * g.split_stride + off] = v;
+  else
+    atomicAdd(dw + off, v);
+}
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgtGeom g, const T* __restrict__ x,
@@ -408,7 +419,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgtGeom g, const T
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * 32 + 16 * i + fq * 4 + r;
-        if (co < g.Co) atomicAdd(dw + (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[i][j][r]);
+        if (co < g.Co) wg_out(g, dw, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[i][j][r]);
       }
     }
 }
@@ -824,7 +835,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_bf16_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + wm * 32 + 16 * i + fq * 4 + r;
-          if (co < g.Co) atomicAdd(dw + (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
+          if (co < g.Co) wg_out(g, dw, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
         }
       }
   }
@@ -1047,7 +1058,7 @@ __global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + wm * WTM + 16 * i + fq * 4 + r;
-          if (co < g.Co) atomicAdd(dw + (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
+          if (co < g.Co) wg_out(g, dw, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
         }
       }
   }
@@ -1892,13 +1903,18 @@ int vd_conv3d_bwd_data(const vd_conv_desc* d, const void* dy, const void* w_bwd,
   });
 }
 
-int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, float* dw,
-                         void* stream) {
+}  // extern "C"
+
+// The weight-gradient launch.  `splits_out` receives the number of pixel splits (grid.y);
+// with dry = true nothing is launched (workspace sizing); split_stride as in WgtGeom.
+static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float* dw,
+                     int64_t split_stride, int64_t* splits_out, bool dry, void* stream) {
   int rc = check_desc(d);
   if (rc) return rc;
-  VD_REQUIRE(x && dy && dw, "null tensor");
+  VD_REQUIRE(dry || (x && dy && dw), "null tensor");
   VD_REQUIRE(d->Co % 8 == 0, "bwd_weight needs Co %% 8 == 0 (got %d)", d->Co);
   WgtGeom g;
+  g.split_stride = split_stride;
   g.B = d->B;
   g.Ti = d->Ti; g.Hi = d->Hi; g.Wi = d->Wi; g.Ci = d->Ci;
   g.xCs = d->x_cstride ? d->x_cstride : d->Ci;
@@ -1966,6 +1982,8 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     if (splits < 1) splits = 1;
     g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
     splits = vd_cdiv(g.M, g.m_per_split);
+    *splits_out = splits;
+    if (dry) return VD_OK;
     dim3 grid((unsigned)tiles, (unsigned)splits);
 #define VD_WGD(RW, COT, NST, ONE, ...)                                                     \
   do {                                                                                     \
@@ -2010,6 +2028,8 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
     if (splits < 1) splits = 1;
     g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
     splits = vd_cdiv(g.M, g.m_per_split);
+    *splits_out = splits;
+    if (dry) return VD_OK;
     dim3 grid((unsigned)tiles, (unsigned)splits);
 #define VD_WG(RW)                                                                        \
   wgrad_bf16_kernel<RW><<<grid, kThreads, 2 * (64 + RW) * 72 * 2, st>>>(                \
@@ -2028,12 +2048,87 @@ int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, f
   if (splits < 1) splits = 1;
   g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 32) * 32;
   splits = vd_cdiv(g.M, g.m_per_split);
+  *splits_out = splits;
+  if (dry) return VD_OK;
   return VD_DISPATCH_DTYPE(d->dtype, T, {
     constexpr int LD = 64 + (sizeof(T) == 2 ? 8 : 4);
     const size_t lds = 2 * 2 * 32 * LD * sizeof(T);
     conv_wgrad_kernel<T><<<dim3((unsigned)tiles, (unsigned)splits), kThreads, lds,
                            VD_STREAM(stream)>>>(g, (const T*)x, (const T*)dy, dw);
   });
+}
+
+// grid (ceil(n4 / 256)): one thread per 4 consecutive ci of one (co, tap) row of the
+// partials part[s][co][tap][ci] (coalesced 16-B loads), summed over the splits in ascending
+// order and written to the torch weight layout out[co][ci][tap] (co < Co_out, ci < Ci_out).
+__global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* __restrict__ part,
+                                                           int splits, int64_t sstride, int Ci,
+                                                           int taps, int Co_out, int Ci_out,
+                                                           float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int ci4 = Ci / 4;
+  const int64_t rows = (int64_t)Co_out * taps;
+  if (i >= rows * ci4) return;
+  const int cq = (int)(i % ci4);
+  const int64_t row = i / ci4;  // co * taps + tap
+  const int tap = (int)(row % taps), co = (int)(row / taps);
+  const int ci = cq * 4;
+  if (ci >= Ci_out) return;
+  const float* p = part + row * Ci + ci;
+  float4 a = *reinterpret_cast<const float4*>(p);
+  for (int sp = 1; sp < splits; ++sp) {
+    const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)sp * sstride);
+    a.x += v.x;
+    a.y += v.y;
+    a.z += v.z;
+    a.w += v.w;
+  }
+  float* o = out + ((int64_t)co * Ci_out + ci) * taps + tap;
+  const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (ci + k < Ci_out) o[(int64_t)k * taps] = av[k];
+}
+
+extern "C" {
+
+int vd_conv3d_bwd_weight(const vd_conv_desc* d, const void* x, const void* dy, float* dw,
+                         void* stream) {
+  int64_t splits = 0;
+  return wgrad_run(d, x, dy, dw, 0, &splits, false, stream);
+}
+
+size_t vd_conv3d_bwd_weight_workspace_size(const vd_conv_desc* d) {
+  int64_t splits = 0;
+  if (!d || wgrad_run(d, nullptr, nullptr, nullptr, 1, &splits, true, nullptr)) return 0;
+  return (size_t)splits * d->Co * d->kt * d->kh * d->kw * d->Ci * sizeof(float) + 256;
+}
+
+int vd_conv3d_bwd_weight_det(const vd_conv_desc* d, const void* x, const void* dy, float* dw,
+                             int Co_out, int Ci_out, void* workspace, size_t workspace_bytes,
+                             void* stream) {
+  int64_t splits = 0;
+  int rc = wgrad_run(d, x, dy, nullptr, 1, &splits, true, stream);
+  if (rc) return rc;
+  VD_REQUIRE(x && dy && dw && workspace, "null tensor");
+  VD_REQUIRE(Co_out > 0 && Co_out <= d->Co && Ci_out > 0 && Ci_out <= d->Ci,
+             "dw extent %dx%d outside the descriptor's %dx%d", Co_out, Ci_out, d->Co, d->Ci);
+  VD_REQUIRE(d->Ci % 4 == 0, "bwd_weight_det needs Ci %% 4 == 0 (got %d)", d->Ci);
+  VD_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "workspace not 16-B aligned");
+  const int taps = d->kt * d->kh * d->kw;
+  const int64_t sstride = (int64_t)d->Co * taps * d->Ci;
+  VD_REQUIRE(workspace_bytes >= (size_t)splits * sstride * sizeof(float),
+             "workspace %zu B < %lld B", workspace_bytes,
+             (long long)(splits * sstride * (int64_t)sizeof(float)));
+  float* part = reinterpret_cast<float*>(workspace);
+  // every split writes every element of its slice (all co / ci tiles x taps, split ranges
+  // non-empty: splits = ceil(M / m_per_split)), so the slices need no clearing
+  rc = wgrad_run(d, x, dy, part, sstride, &splits, false, stream);
+  if (rc) return rc;
+  const int64_t n4 = (int64_t)Co_out * taps * (d->Ci / 4);
+  wgrad_finish_kernel<<<(unsigned)vd_cdiv(n4, 256), 256, 0, VD_STREAM(stream)>>>(
+      part, (int)splits, sstride, d->Ci, taps, Co_out, Ci_out, dw);
+  return vd::check_launch("conv_wgrad_finish");
 }
 
 }  // extern "C"

@@ -16,6 +16,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kVec = 8;             // channels per lane
 constexpr int kTargetChunks = 2048; // workgroups per launch (B * nchunk)
+constexpr int kSumPer = 64;         // chunk partials per gn_bwd_sum_kernel workgroup
 
 struct GNPlan {
   int rows_per_iter;  // pixel rows a WG covers per iteration
@@ -212,12 +213,8 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
     int64_t S, int C, int G, int64_t chunk_px, int rows_per_iter, float* __restrict__ part,
-    Drop drop_in, float* __restrict__ zero, int nzero) {
+    Drop drop_in) {
   const Drop drop = drop_in.resolved();
-  // the first workgroup clears gn_bwd_sum_kernel's atomic targets (it runs after this kernel
-  // in stream order): no separate memset launch
-  if (blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0.f;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* sh = reinterpret_cast<float2*>(smem);  // [rows_per_iter][C]
   const int nvec = C / kVec;
@@ -274,13 +271,14 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
   }
 }
 
-// grid (ceil(C/64), B), 1024 threads = 64 channels x 16 chunk lanes: per-(b, c) sums of
-// the chunk partials -> sums[b][c][2] (coalesced 512-B rows, 16-way parallel over chunks)
+// grid (ceil(C/64), B, ksplit), 1024 threads = 64 channels x 16 chunk lanes: per-(b, c) sums
+// of the chunk partials (coalesced 512-B rows, 16-way parallel over chunks).  Workgroup z sums
+// chunks [z * kper, (z + 1) * kper) in a fixed order and WRITES sums[z][b][c][2]; the finalize
+// kernel adds the ksplit slices in order.  No atomics: the backward is bit-reproducible
+// (the same-address float atomics of round 3 summed in arrival order).
 __global__ __launch_bounds__(1024) void gn_bwd_sum_kernel(const float* __restrict__ part,
                                                           int nchunk, int C, int kper,
                                                           float* __restrict__ sums) {
-  // grid (C / 64, B, splits): this WG sums chunks [z * kper, (z + 1) * kper) and adds into
-  // sums (zeroed by gn_bwd_reduce_kernel) -- enough workgroups to stream the partials at speed
   __shared__ float2 sh[16][64];
   const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
@@ -302,16 +300,29 @@ __global__ __launch_bounds__(1024) void gn_bwd_sum_kernel(const float* __restric
       a.x += sh[k][cl].x;
       a.y += sh[k][cl].y;
     }
-    atomicAdd(sums + ((int64_t)b * C + c) * 2, a.x);
-    atomicAdd(sums + ((int64_t)b * C + c) * 2 + 1, a.y);
+    float* o = sums + (((int64_t)blockIdx.z * gridDim.y + b) * C + c) * 2;
+    o[0] = a.x;
+    o[1] = a.y;
   }
 }
 
-// one WG: group coefficients per (b, g) and dgamma/dbeta per channel from sums[b][c][2]
-__global__ void gn_bwd_finalize_kernel(const float* __restrict__ sums, int B, int C, int G,
+// one WG: the ksplit slices of sums[z][b][c][2] added in order into slice 0, then group
+// coefficients per (b, g) and dgamma/dbeta per channel
+__global__ void gn_bwd_finalize_kernel(float* __restrict__ sums, int ksplit, int B, int C, int G,
                                        int64_t S, const float* __restrict__ gamma,
                                        float* __restrict__ coef, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta) {
+  const int64_t slice = (int64_t)B * C * 2;
+  for (int i = threadIdx.x; i < B * C; i += blockDim.x) {
+    float a = sums[2 * i], s = sums[2 * i + 1];
+    for (int z = 1; z < ksplit; ++z) {
+      a += sums[z * slice + 2 * i];
+      s += sums[z * slice + 2 * i + 1];
+    }
+    sums[2 * i] = a;
+    sums[2 * i + 1] = s;
+  }
+  __syncthreads();
   const int cpg = C / G;
   const float inv_n = 1.f / ((float)cpg * (float)S);
   for (int bg = threadIdx.x; bg < B * G; bg += blockDim.x) {
@@ -403,7 +414,8 @@ size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G) {
   if (B <= 0 || S <= 0 || C <= 0 || G <= 0 || C % kVec) return 0;
   GNPlan p = gn_plan(B, S, C);
   size_t fwd = (size_t)B * p.nchunk * G * 3 * sizeof(float);
-  size_t bwd = ((size_t)B * p.nchunk * C * 2 + (size_t)B * G * 2 + (size_t)B * C * 2) *
+  const size_t ksplit = vd_cdiv(p.nchunk, kSumPer);
+  size_t bwd = ((size_t)B * p.nchunk * C * 2 + (size_t)B * G * 2 + ksplit * B * C * 2) *
                sizeof(float);
   return (fwd > bwd ? fwd : bwd) + 256;
 }
@@ -461,15 +473,16 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
     if (silu)
       gn_bwd_reduce_kernel<T, true><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part, drop, sums, B * C * 2);
+          p.rows_per_iter, part, drop);
     else
       gn_bwd_reduce_kernel<T, false><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part, drop, sums, B * C * 2);
-    const int kper = 64, ksplit = (int)vd_cdiv(p.nchunk, kper);
+          p.rows_per_iter, part, drop);
+    const int ksplit = (int)vd_cdiv(p.nchunk, kSumPer);
     gn_bwd_sum_kernel<<<dim3((unsigned)vd_cdiv(C, 64), B, ksplit), 1024, 0, st>>>(
-        part, p.nchunk, C, kper, sums);
-    gn_bwd_finalize_kernel<<<1, kThreads, 0, st>>>(sums, B, C, G, S, gamma, coef, dgamma, dbeta);
+        part, p.nchunk, C, kSumPer, sums);
+    gn_bwd_finalize_kernel<<<1, kThreads, 0, st>>>(sums, ksplit, B, C, G, S, gamma, coef, dgamma,
+                                                   dbeta);
     if (silu)
       gn_bwd_apply_kernel<T, true><<<grid, kThreads, 0, st>>>(
           (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,

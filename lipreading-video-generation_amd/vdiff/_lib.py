@@ -66,7 +66,9 @@ _SIGS = {
     "vd_silu": (_i, [_vp, _vp, _i64, _i, _vp]),
     "vd_silu_bwd": (_i, [_vp, _vp, _vp, _i64, _i, _vp]),
     "vd_cond_concat": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
-    "vd_cond_concat_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "vd_cond_concat_bwd_workspace_size": (_sz, [_i, _i, _i, _i, _i]),
+    "vd_cond_concat_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
+                                _vp]),
     "vd_upsample_nearest_hw": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),
     "vd_upsample_nearest_hw_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp]),
     "vd_channel_sums_workspace_size": (_sz, [_i, _i]),
@@ -77,6 +79,8 @@ _SIGS = {
     "vd_conv3d_fwd": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "vd_conv3d_bwd_data": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp]),
     "vd_conv3d_bwd_weight": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp]),
+    "vd_conv3d_bwd_weight_workspace_size": (_sz, [C.POINTER(ConvDesc)]),
+    "vd_conv3d_bwd_weight_det": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _i, _i, _vp, _sz, _vp]),
     "vd_attention_fwd": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp]),
     "vd_attention_fwd_workspace_size": (_sz, [C.POINTER(AttnDesc)]),
     "vd_attention_fwd_ws": (_i, [C.POINTER(AttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),

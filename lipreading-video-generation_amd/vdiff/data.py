@@ -185,8 +185,15 @@ def _device_error(e: BaseException) -> bool:
     """A HIP/CUDA initialisation or launch failure: never swallowed into (None, None) (a
     forked DataLoader worker cannot re-initialise the GPU; hiding that only moves the error
     to collate)."""
+    if not isinstance(e, RuntimeError):
+        return False
     msg = str(e)
-    return isinstance(e, RuntimeError) and any(k in msg for k in ("CUDA", "HIP", "hip", "cuda"))
+    # specific markers only: a bare "hip" / "cuda" substring also matches paths such as
+    # .../ship/... or .../barracuda/... of an ordinary per-item data error
+    markers = ("HIP error", "hipError", "CUDA error", "CUDA driver", "CUDA out of memory",
+               "HIP out of memory", "Cannot re-initialize CUDA", "no CUDA GPUs",
+               "Found no NVIDIA driver", "libvdiff ", "libvdiff.so", "device-side assert")
+    return any(k in msg for k in markers)
 
 
 class TalkingFaceFrameDataset(torch.utils.data.Dataset):

@@ -143,12 +143,31 @@ class Trainer:
             self.check_finite()
 
     def check_finite(self):
-        """Raise FloatingPointError if any step so far had a non-finite loss (host sync)."""
-        if self._first_bad is not None:
-            first = int(self._first_bad)
-            if first >= 0:
-                raise FloatingPointError(f"non-finite training loss at step {first} "
-                                         f"(of {self.steps_done})")
+        """Raise FloatingPointError if any step so far had a non-finite loss (host sync).
+
+        Under DDP (the gradient bucketer active) the first bad step is MIN-all-reduced over
+        the ranks first, so a loss that went non-finite on one rank makes EVERY rank raise
+        here together instead of leaving the others blocked in the next gradient
+        all-reduce (advisor r03).  Every rank reaches this call at the same step count."""
+        if self._first_bad is None and self.bucketer is None:
+            return
+        if self._first_bad is None:
+            dev = next(self.model.parameters()).device
+            self._first_bad = torch.full((), -1, dtype=torch.int64, device=dev)
+        fb = self._first_bad
+        if self.bucketer is not None:
+            big = torch.iinfo(torch.int64).max
+            v = torch.where(fb >= 0, fb, torch.full_like(fb, big)).reshape(1)
+            if v.is_cuda and torch.distributed.get_backend() == "gloo":
+                v = v.cpu()
+            torch.distributed.all_reduce(v, op=torch.distributed.ReduceOp.MIN)
+            first = int(v[0])
+            first = -1 if first == big else first
+        else:
+            first = int(fb)
+        if first >= 0:
+            raise FloatingPointError(f"non-finite training loss at step {first} "
+                                     f"(of {self.steps_done})")
 
 
 class TrainStepGraph:

@@ -11,6 +11,7 @@ libvdiff.so raises.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -19,6 +20,9 @@ from . import _lib
 from ._lib import AttnDesc, ConvDesc, VD_BF16, VD_F32, XAttnDesc
 
 _DT = {torch.float32: VD_F32, torch.bfloat16: VD_BF16}
+# A/B knob: VDIFF_WGRAD_ATOMIC=1 restores round 3's split-K float atomics for the conv weight
+# gradient (run-to-run non-reproducible); the default is the fixed-order split-K
+_WGRAD_ATOMIC = os.environ.get("VDIFF_WGRAD_ATOMIC", "0") == "1"
 
 
 # --------------------------------------------------------------------- helpers
@@ -374,8 +378,10 @@ class CondConcatFn(torch.autograd.Function):
         dout = to_cl(dout)
         d_imc = torch.empty(B, h, w, Ci, dtype=torch.float32, device=dout.device)
         d_aud = torch.empty(B, T, Ca, dtype=torch.float32, device=dout.device)
+        ws = torch.empty(_lib.lib().vd_cond_concat_bwd_workspace_size(B, T, H, W, max(Ca, 1)),
+                         dtype=torch.uint8, device=dout.device)
         _lib.call("vd_cond_concat_bwd", _p(dout), _p(d_imc), _p(d_aud), B, T, H, W, Cx, h, w, Ci,
-                  Ca, cs, _dtype(dout), _stream(dout))
+                  Ca, cs, _dtype(dout), _p(ws), _stream(dout))
         d_img = dout[:, :Cx]
         return d_img, d_imc.permute(0, 3, 1, 2).to(idt), d_aud.to(adt), None
 
@@ -703,13 +709,23 @@ class ConvFn(torch.autograd.Function):
                                 _conv_flop(B, out, Co, k, Ci))
             dx = dxp[:, :Ci] if Cip != Ci else dxp
         if ctx.needs_input_grad[1]:
-            dwp = torch.zeros(Cop, taps, Cip, dtype=torch.float32, device=dy.device)
             ev = _timer.begin() if _timer is not None and _timer.convs else None
-            _lib.call("vd_conv3d_bwd_weight", d, _p(xp), _p(dyp), _p(dwp), st)
+            if _WGRAD_ATOMIC:  # A/B: round-3 split-K atomics (not bit-reproducible)
+                dwp = torch.zeros(Cop, taps, Cip, dtype=torch.float32, device=dy.device)
+                _lib.call("vd_conv3d_bwd_weight", d, _p(xp), _p(dyp), _p(dwp), st)
+                dw = dwp[:Co, :, :Ci].permute(0, 2, 1).reshape(weight.shape)
+            else:
+                # fixed-order split-K: partials per pixel split, one ordered pass writes dW
+                # straight into the torch layout (no zero fill, no permute copy)
+                dw = torch.empty(weight.shape, dtype=torch.float32, device=dy.device)
+                ws = torch.empty(_lib.lib().vd_conv3d_bwd_weight_workspace_size(d),
+                                 dtype=torch.uint8, device=dy.device)
+                _lib.call("vd_conv3d_bwd_weight_det", d, _p(xp), _p(dyp), _p(dw), Co, Ci,
+                          _p(ws), ws.numel(), st)
             if ev is not None:
                 _timer.end_conv(ev, "conv_bwd_weight", _conv_key(Cip, Co, k, s, out),
                                 _conv_flop(B, out, Co, k, Ci))
-            dw = dwp[:Co, :, :Ci].permute(0, 2, 1).reshape(weight.shape).to(weight.dtype)
+            dw = dw.to(weight.dtype)
         want_b = has_b and ctx.needs_input_grad[2]
         want_ca = has_ca and ctx.needs_input_grad[3]
         if want_b or want_ca:

@@ -47,6 +47,17 @@ def train_step_inputs(T=8, S=64):
             seeded((T, 64), 72), seeded((1, 3, T, S, S), 73))
 
 
+TRAIN5_T = (37, 5, 80, 62, 19)  # injected timesteps of the five-step fixture (train.py:125)
+
+
+def train5_inputs(k, T=8, S=64):
+    """Seeded inputs of step k of the five-step fixture (tests/golden/train_steps5_tiny3d.npz):
+    x0, cond image, pooled audio features [T, 64], eps."""
+    return (seeded((1, 3, T, S, S), 500 + 10 * k, "uniform"),
+            seeded((1, 3, 32, 32), 501 + 10 * k, "uniform"),
+            seeded((T, 64), 502 + 10 * k), seeded((1, 3, T, S, S), 503 + 10 * k))
+
+
 def adam_delta_close(delta, delta_ref, grad_ref, lr=1e-2):
     """One Adam step from zero state moves each parameter by -lr * g / (|g| + 1e-8), i.e.
     ~ -lr * sign(g): compare where that is insensitive to the gradient's own rounding

@@ -35,7 +35,8 @@ import noise_scheduler as ref_ns  # noqa: E402
 import unet as ref_unet  # noqa: E402
 import utils as ref_utils  # noqa: E402
 
-from oracle.fixtures import FULL2D, FULL2D_SHAPE, TINY3D, TINY3D_SHAPE, seeded  # noqa: E402
+from oracle.fixtures import (FULL2D, FULL2D_SHAPE, TINY3D, TINY3D_SHAPE, TRAIN5_T,  # noqa: E402
+                             seeded, train5_inputs)
 from oracle.unet import audio_param_shapes, build_plan, init_params, param_shapes  # noqa: E402
 
 torch.set_num_threads(8)
@@ -319,6 +320,62 @@ def gen_train_step():
     save("train_step_tiny3d.npz", **out)
 
 
+# ------------------------------------------------------------------ five train steps
+def gen_train_steps5():
+    """Five consecutive steps of the reference training loop (train.py:107-134) on BASELINE
+    config 1's shape: ONE torch.optim.Adam(lr=1e-2) over the imported reference UNetModel plus
+    the restated conditioning (as gen_train_step), a new seeded batch, noise and timestep per
+    step.  Saves every step's loss, the step-1 and step-5 gradients and the five-step
+    parameter change of selected parameters: the pin of the product Trainer beyond one step
+    (the product packs its conv operands per call in step 1 and in one
+    batched launch from step 2 on)."""
+    m = ref_unet.UNetModel(image_size=64, **TINY3D)
+    m.train()
+    load_init(m, 1234)
+    A = init_params(audio_param_shapes(64, 16, im_cond_output_ch=16), 77)
+    lin = nn.Linear(64, 16)
+    lin.weight.data.copy_(A["audio_transformer.transform.0.weight"])
+    lin.bias.data.copy_(A["audio_transformer.transform.0.bias"])
+    cc = nn.Conv2d(3, 16, 1, bias=False)
+    cc.weight.data.copy_(A["cond_conv_in.weight"])
+    T, S = TINY3D_SHAPE[2], TINY3D_SHAPE[3]
+    sched = ref_lns.LinearNoiseScheduler(100, 0.00085, 0.012)
+    params = list(m.parameters()) + list(lin.parameters()) + list(cc.parameters())
+    names = [n for n, _ in m.named_parameters()] + \
+        ["audio_transformer.transform.0.weight", "audio_transformer.transform.0.bias",
+         "cond_conv_in.weight"]
+    before = [p.detach().clone() for p in params]
+    opt = torch.optim.Adam(params, 1e-2)  # train.py:102
+    sel = ("input_blocks.0.0.weight", "out.2.weight", "input_blocks.3.1.qkv.weight",
+           "input_blocks.3.1.proj_out.weight", "middle_block.0.in_layers.0.weight",
+           "output_blocks.0.0.skip_connection.weight", "time_embed.0.weight",
+           "audio_transformer.transform.0.weight", "cond_conv_in.weight")
+    out = {"t": torch.tensor(TRAIN5_T)}
+    losses = []
+    for k, tk in enumerate(TRAIN5_T):
+        x0, cond, feat, eps = train5_inputs(k, T, S)
+        t = torch.tensor([tk])
+        opt.zero_grad()
+        xt = sched.add_noise(x0, eps, t)
+        a = F.relu(lin(feat)).reshape(1, T, 16).permute(0, 2, 1).reshape(1, 16, T, 1, 1)
+        a = a.expand(-1, -1, -1, S, S)
+        imc = cc(F.interpolate(cond, size=(S, S))).unsqueeze(2).expand(-1, -1, T, -1, -1)
+        y = m(torch.cat([xt, imc, a], dim=1), t)
+        loss = nn.MSELoss()(y, eps)
+        loss.backward()
+        losses.append(float(loss))
+        if k in (0, 4):
+            for n, p in zip(names, params):
+                if n in sel:
+                    out[f"grad{k + 1}_{n}"] = p.grad.detach().clone()
+        opt.step()
+    out["losses"] = torch.tensor(losses)
+    for n, p, b in zip(names, params, before):
+        if n in sel:
+            out["delta5_" + n] = p.detach() - b
+    save("train_steps5_tiny3d.npz", **out)
+
+
 # ------------------------------------------------------------------ sampling trajectories
 TRAJ_STEPS = 10
 TRAJ_KEEP = (1, 5, 10)  # steps whose x_t / x0 are stored
@@ -412,7 +469,8 @@ def gen_trajectory():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["schedulers", "blocks", "models", "train_step", "trajectory"]
+    which = sys.argv[1:] or ["schedulers", "blocks", "models", "train_step", "train_steps5",
+                             "trajectory"]
     if "schedulers" in which:
         gen_schedulers()
     if "blocks" in which:
@@ -421,5 +479,7 @@ if __name__ == "__main__":
         gen_models()
     if "train_step" in which:
         gen_train_step()
+    if "train_steps5" in which:
+        gen_train_steps5()
     if "trajectory" in which:
         gen_trajectory()

@@ -123,3 +123,16 @@ def test_dataset_returns_raw_frames_without_transforms(tmp_path):
     np.testing.assert_array_equal(ds2[3][1], frames[out_idx][::2, ::2])
     assert vd.TalkingFaceFrameDataset([vd.FrameItem(str(tmp_path / "no.vdclip"), 0, 1)])[0] \
         == (None, None)
+
+
+def test_device_error_markers():
+    """Advisor r03: only real HIP / CUDA / libvdiff failures propagate out of a dataset item;
+    an ordinary data error whose message merely contains "hip" / "cuda" (a path such as
+    /data/ship/clip.vdclip) is a per-item error (None, None) as in the reference."""
+    from vdiff.data import _device_error
+    assert _device_error(RuntimeError("HIP error: invalid device function"))
+    assert _device_error(RuntimeError("CUDA error: out of memory"))
+    assert _device_error(RuntimeError("libvdiff vd_frames_resize_normalize failed (code 3): x"))
+    assert not _device_error(RuntimeError("cannot open /data/ship/clip_0001.vdclip"))
+    assert not _device_error(RuntimeError("bad header in /mnt/barracuda/x.vdclip"))
+    assert not _device_error(ValueError("HIP error"))

@@ -152,3 +152,62 @@ def test_conv1x1_fused_epilogue(dtype):
     assert rel_l2(y, yr) < tol
     for a, r in zip(dl, leaves):
         assert rel_l2(a.grad, r.grad) < 2 * tol + 1e-5
+
+
+def _wgrad(x, w, dy, stride, pad, atomic):
+    from vdiff import ops
+    old = ops._WGRAD_ATOMIC
+    ops._WGRAD_ATOMIC = atomic
+    try:
+        xd = x.detach().requires_grad_(False)
+        wd = w.detach().clone().requires_grad_(True)
+        y = ops.conv(xd, wd, None, stride=stride, padding=pad)
+        y.backward(dy)
+        return wd.grad
+    finally:
+        ops._WGRAD_ATOMIC = old
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_conv_wgrad_fixed_order(case, dtype):
+    """the default weight gradient (per-split partials + one ordered pass,
+    vd_conv3d_bwd_weight_det) is bit-identical run to run and equals round 3's atomic split-K
+    kernel up to fp32 summation order (both are checked against the oracle above)."""
+    from vdiff import ops
+    shape, Co, k, stride, pad = CASES[case]
+    nd = len(shape) - 2
+    x = ops.to_cl(seeded(shape, 100 + case).to(dev, dtype))
+    w, _ = _weights(shape[1], Co, k, nd, 200 + case)
+    w = w.to(dev)
+    y = ops.conv(x, w, None, stride=stride, padding=pad)
+    dy = ops.to_cl(seeded(tuple(y.shape), 300 + case).to(dev, dtype))
+    a = _wgrad(x, w, dy, stride, pad, False)
+    b = _wgrad(x, w, dy, stride, pad, False)
+    c = _wgrad(x, w, dy, stride, pad, True)
+    assert torch.equal(a, b)
+    assert rel_l2(a, c) < 1e-6, rel_l2(a, c)
+
+
+@pytest.mark.parametrize("shape,Co,k", [((1, 64, 16, 128, 128), 64, 3),
+                                       ((1, 256, 16, 32, 32), 256, 3),
+                                       ((1, 64, 16, 128, 128), 192, 1)])
+def test_conv_wgrad_fixed_order_config2(shape, Co, k):
+    """Config-2 weight-gradient shapes, where the split-K has 8-256 pixel splits (the atomic
+    kernel's sums then depend on arrival order): two fixed-order runs are bit-identical, and
+    they agree with the atomic kernel and with a torch fp32 conv weight gradient of the same
+    bf16 operands."""
+    from vdiff import ops
+    x = ops.to_cl(seeded(shape, 7).to(dev, torch.bfloat16))
+    w = (seeded((Co, shape[1]) + (k,) * 3, 8) / (shape[1] * k ** 3) ** 0.5).to(dev)
+    pad = k // 2
+    y = ops.conv(x, w, None, padding=pad)
+    dy = ops.to_cl(seeded(tuple(y.shape), 9).to(dev, torch.bfloat16))
+    a = _wgrad(x, w, dy, 1, pad, False)
+    b = _wgrad(x, w, dy, 1, pad, False)
+    c = _wgrad(x, w, dy, 1, pad, True)
+    assert torch.equal(a, b)
+    assert rel_l2(a, c) < 1e-5, rel_l2(a, c)
+    ref = torch.nn.grad.conv3d_weight(x.float().cpu().contiguous(), w.shape,
+                                      dy.float().cpu().contiguous(), padding=pad)
+    assert rel_l2(a, ref) < 1e-4, rel_l2(a, ref)

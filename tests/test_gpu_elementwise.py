@@ -184,3 +184,37 @@ def test_cond_concat_matches_torch(dtype, five, cpad):
         ref = F.pad(ref, [0, 0] * (ref.dim() - 2) + [0, cs - ref.shape[1]])
     out = ops.cond_concat(img.to(dev), imc.to(dev), aud.to(dev), cpad=cpad)
     assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hw", [(5, 7), (12, 10), (4, 5)])
+def test_cond_concat_bwd_matches_torch(dtype, hw):
+    """vd_cond_concat_bwd: d_imc (the adjoint of the nearest resize, summed over T) and d_audio
+    (summed over H x W) against torch autograd of the same composition; fixed-order sums, so
+    two runs are bit-identical (round 3 added the chunk partials with float atomics)."""
+    import torch.nn.functional as F
+    from vdiff import ops
+    B, T, H, W, Cx, Ci, Ca = 2, 3, 12, 10, 3, 16, 24
+    h, w = hw
+    g = torch.Generator().manual_seed(6)
+    img = torch.randn((B, Cx, T, H, W), generator=g).to(dtype)
+    imc = torch.randn(B, Ci, h, w, generator=g).to(dtype)
+    aud = torch.randn(B, T, Ca, generator=g).to(dtype)
+    gout = torch.randn((B, 200, T, H, W), generator=g).to(dtype)
+    ir, ar = imc.float().requires_grad_(True), aud.float().requires_grad_(True)
+    ic = F.interpolate(ir, size=(H, W), mode="nearest")[:, :, None].expand(B, Ci, T, H, W)
+    au = ar.permute(0, 2, 1)[:, :, :, None, None].expand(B, Ca, T, H, W)
+    ref = torch.cat([img.float(), ic, au], 1)
+    ref = F.pad(ref, [0, 0, 0, 0, 0, 0, 0, 200 - ref.shape[1]])
+    ref.backward(gout.float())
+    outs = []
+    for _ in range(2):
+        i_d = imc.to(dev).requires_grad_(True)
+        a_d = aud.to(dev).requires_grad_(True)
+        out = ops.cond_concat(img.to(dev), i_d, a_d, cpad=200)
+        out.backward(ops.to_cl(gout.to(dev)))
+        outs.append((i_d.grad.float().cpu(), a_d.grad.float().cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert rel_l2(outs[0][0], ir.grad) < tol, rel_l2(outs[0][0], ir.grad)
+    assert rel_l2(outs[0][1], ar.grad) < tol, rel_l2(outs[0][1], ar.grad)

@@ -195,6 +195,30 @@ def test_one_adam_train_step():
         assert adam_delta_close(deltas[k], g["delta_" + k], g["grad_" + k]) < 1e-6, k
 
 
+def test_five_adam_train_steps():
+    """the oracle's training loop (one Adam over five steps, a new seeded
+    batch / noise / t per step) against the reference's (train.py:107-134, imported by
+    tests/golden/gen_golden.py gen_train_steps5): losses, step-1 / step-5 gradients and the
+    five-step parameter change."""
+    from oracle.fixtures import TRAIN5_T, train5_inputs
+    from oracle.train import train_steps
+    g = golden("train_steps5_tiny3d.npz")
+    assert tuple(g["t"].tolist()) == TRAIN5_T
+    plan = build_plan(**TINY3D)
+    P = init_params(param_shapes(plan), 1234)
+    P.update(init_params(audio_param_shapes(64, 16, im_cond_output_ch=16), 77))
+    P0 = {k: v.clone() for k, v in P.items()}
+    batches = [train5_inputs(k) + (torch.tensor([t]),) for k, t in enumerate(TRAIN5_T)]
+    losses, kept = train_steps(P, plan, batches, 16, keep_grads=(0, 4))
+    close(losses, g["losses"], atol=1e-6, rtol=1e-5)
+    names = [k[len("delta5_"):] for k in g if k.startswith("delta5_")]
+    assert len(names) == 9
+    for k in names:
+        assert rel_l2(kept[0][k], g["grad1_" + k]) < 1e-5, k
+        assert rel_l2(kept[4][k], g["grad5_" + k]) < 1e-5, k
+        assert rel_l2(P[k] - P0[k], g["delta5_" + k]) < 1e-5, k
+
+
 def test_cross_attention_oracle_reduces_to_reference():
     """Pins oracle.nn.cross_attention (the audio cross-attention restatement, no reference
     counterpart) to the reference's attention math: with each frame's own k / v tokens as

@@ -50,3 +50,46 @@ def test_check_finite_between_reads_and_disabled():
     off = Trainer(_Model({0}), _Sched(), lr=1e-3, check_every=0)
     off.step(c)
     off.check_finite()
+
+
+def _ddp_worker(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from vdiff.ddp import broadcast_parameters, init_from_env
+    init_from_env("gloo")
+    torch.manual_seed(0)
+    m = _Model({2} if rank == 1 else set())  # rank 1 alone goes non-finite at step 2
+    broadcast_parameters(m)
+    tr = Trainer(m, _Sched(), lr=1e-3, check_every=4)
+    c = _clip()
+    res = "no raise"
+    try:
+        for _ in range(6):
+            tr.step(c)
+    except FloatingPointError as e:
+        res = f"raised after {tr.steps_done} steps: {e}"
+    q.put((rank, res))
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_nonfinite_loss_raises_on_every_rank():
+    """Advisor r03: a loss that goes non-finite on ONE rank makes every rank raise at the same
+    read (the first bad step is MIN-all-reduced), so no rank is left waiting in the next
+    gradient all-reduce.  world_size 2 over gloo."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert got[r].startswith("raised after 4 steps") and "step 2 " in got[r], got
