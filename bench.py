@@ -419,6 +419,7 @@ def graph_leg(args, device):
     from vdiff.engine import Trainer, synthetic_clip
     from vdiff.schedulers import LinearNoiseScheduler
     trainers = {}
+    os.environ["VDIFF_TRAIN_GRAPH_EXPERIMENTAL"] = "1"  # --train-graph is the explicit opt-in
     for mode in ("eager", "graph"):
         torch.manual_seed(1234)
         model = build_model(args, device)

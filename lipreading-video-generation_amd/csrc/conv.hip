@@ -268,12 +268,33 @@ struct WgtGeom {
   // 0: atomicAdd into dw (vd_conv3d_bwd_weight).  > 0: split y WRITES its partial dW to
   // dw + y * split_stride (vd_conv3d_bwd_weight_det; summed in a fixed order afterwards)
   int64_t split_stride;
+  // XCD-aware 1-D grid (wgrad_dma_kernel): xcd_tiles > 0 = the (tile, split) pairs in
+  // split-major order are laid out so that each XCD runs a contiguous range of them, i.e.
+  // all tiles of one pixel split on ONE XCD, whose L2 then serves the split's dY rows and X
+  // strips to every tile (MI355X: workgroup b runs on XCD b % 8, each XCD has its own L2).
+  int xcd_tiles, xcd_total;
 };
 
+// (tile, split) of this workgroup
+__device__ __forceinline__ bool wg_tile(const WgtGeom& g, int* tile, int* split) {
+  if (g.xcd_tiles == 0) {
+    *tile = blockIdx.x;
+    *split = blockIdx.y;
+    return true;
+  }
+  const int per = gridDim.x / 8;
+  const int L = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (L >= g.xcd_total) return false;
+  *tile = L % g.xcd_tiles;
+  *split = L / g.xcd_tiles;
+  return true;
+}
+
 // one fp32 partial of dW: accumulated (atomics) or stored into the split's own slice
-__device__ __forceinline__ void wg_out(const WgtGeom& g, float* dw, int64_t off, float v) {
+__device__ __forceinline__ void wg_out(const WgtGeom& g, float* dw, int split, int64_t off,
+                                       float v) {
   if (g.split_stride)
-    dw[(int64_t)blockIdx.y * g.split_stride + off] = v;
+    dw[(int64_t)split * g.split_stride + off] = v;
   else
     atomicAdd(dw + off, v);
 }
@@ -419,7 +440,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgtGeom g, const T
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * 32 + 16 * i + fq * 4 + r;
-        if (co < g.Co) wg_out(g, dw, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[i][j][r]);
+        if (co < g.Co) wg_out(g, dw, blockIdx.y, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[i][j][r]);
       }
     }
 }
@@ -835,7 +856,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_bf16_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + wm * 32 + 16 * i + fq * 4 + r;
-          if (co < g.Co) wg_out(g, dw, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
+          if (co < g.Co) wg_out(g, dw, blockIdx.y, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
         }
       }
   }
@@ -875,13 +896,14 @@ __global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
   const bf16_t* lds = reinterpret_cast<const bf16_t*>(smem);
 
   const int co_tiles = (g.Co + COT - 1) / COT, ci_tiles = (g.Ci + 63) / 64;
-  int bid = blockIdx.x;
+  int bid, wsplit;
+  if (!wg_tile(g, &bid, &wsplit)) return;  // padding of the XCD-aware grid
   const int cot = bid % co_tiles; bid /= co_tiles;
   const int cit = bid % ci_tiles; bid /= ci_tiles;
   const int tab = bid;  // PLANE: kt index; otherwise (kt, kh) index
   const int ta = PLANE ? tab : tab / g.kh, tb = PLANE ? 0 : tab % g.kh;
   const int co0 = cot * COT, ci0 = cit * 64;
-  const int64_t mbeg = (int64_t)blockIdx.y * g.m_per_split;
+  const int64_t mbeg = (int64_t)wsplit * g.m_per_split;
   int64_t mend = mbeg + g.m_per_split;
   if (mend > g.M) mend = g.M;
   if (mbeg >= mend) return;
@@ -1058,7 +1080,7 @@ __global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + wm * WTM + 16 * i + fq * 4 + r;
-          if (co < g.Co) wg_out(g, dw, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
+          if (co < g.Co) wg_out(g, dw, wsplit, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, acc[tc][i][j][r]);
         }
       }
   }
@@ -1915,6 +1937,7 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
   VD_REQUIRE(d->Co % 8 == 0, "bwd_weight needs Co %% 8 == 0 (got %d)", d->Co);
   WgtGeom g;
   g.split_stride = split_stride;
+  g.xcd_tiles = g.xcd_total = 0;
   g.B = d->B;
   g.Ti = d->Ti; g.Hi = d->Hi; g.Wi = d->Wi; g.Ci = d->Ci;
   g.xCs = d->x_cstride ? d->x_cstride : d->Ci;
@@ -1985,6 +2008,16 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     *splits_out = splits;
     if (dry) return VD_OK;
     dim3 grid((unsigned)tiles, (unsigned)splits);
+    // XCD-aware 1-D grid (A/B knob VDIFF_WGRAD_XCD=0 restores the 2-D grid)
+    static const int wxcd = [] {
+      const char* e = getenv("VDIFF_WGRAD_XCD");
+      return e ? atoi(e) : 1;
+    }();
+    if (wxcd && tiles > 1) {
+      g.xcd_tiles = (int)tiles;
+      g.xcd_total = (int)(tiles * splits);
+      grid = dim3((unsigned)vd_cdiv(tiles * splits, 8) * 8, 1);
+    }
 #define VD_WGD(RW, COT, NST, ONE, ...)                                                     \
   do {                                                                                     \
     auto kern = wgrad_dma_kernel<RW, COT, NST, ONE, ##__VA_ARGS__>;                        \

@@ -98,11 +98,11 @@ class Trainer:
         if graph and not batch_pack:
             raise ValueError("Trainer(graph=True) needs batch_pack (per-call packs would be "
                              "frozen into the graph)")
-        if graph:
-            warnings.warn("Trainer(graph=True) is experimental: at the config-2 scale (bf16, "
-                          "dropout 0.1, wav2vec2-base, lr 1e-2) replays returned negative / "
-                          "non-finite losses (DESIGN section 9 item 3); small models match the "
-                          "eager step")
+        if graph and os.environ.get("VDIFF_TRAIN_GRAPH_EXPERIMENTAL") != "1":
+            # advisor r03: a known defect must not be one keyword away from a user
+            raise RuntimeError("Trainer(graph=True) is experimental: at the config-2 scale its "
+                               "replays returned negative / non-finite losses (DESIGN section 9 "
+                               "item 3); set VDIFF_TRAIN_GRAPH_EXPERIMENTAL=1 to run it anyway")
         self.graph = TrainStepGraph(self) if graph else None
 
     def step(self, clip: Clip) -> torch.Tensor:
@@ -270,6 +270,7 @@ class TrainStepGraph:
         finally:
             lib.vd_set_dropout_counter(None)
         self.shapes = self._shapes(clip, enc)
+        tr.packs.frozen = True  # the graph replays the pack launch into these buffers
         self.grads = [(p, p.grad) for p in model.parameters() if p.grad is not None]
         missing = [n for n, p in model.named_parameters()
                    if p.requires_grad and id(p) not in enc_ids and p.grad is None]

@@ -492,12 +492,18 @@ class step_packed_weights:
         self.plans = []    # [(dt, desc table (device uint8), n, total)]
         self.dirty = False
         self.active = False
+        # set while a captured HIP graph (engine.TrainStepGraph) reads self.bufs and replays
+        # the pack launch: the plan may then neither be dropped nor rebuilt (advisor r03)
+        self.frozen = False
 
     def __enter__(self):
         global _step_pack
         if self.plans and any(spec[0].data_ptr() != k[1] for k, spec in self.want.items()):
             # a planned weight's storage moved or was freed since the plan was built (.to(),
             # load_state_dict(assign=True), .data = ...): never read the old pointer
+            if self.frozen:
+                raise RuntimeError("a weight's storage moved while a captured train-step graph "
+                                   "reads the packed-operand plan: build a new Trainer")
             self.bufs, self.plans, self.dirty = {}, [], True
         if self.plans:
             for dt, table, n, total in self.plans:
@@ -522,6 +528,8 @@ class step_packed_weights:
         return self.bufs.get(key) if self.plans else None
 
     def record(self, key, spec):
+        if self.frozen:  # served by a per-call pack; the captured plan stays as it is
+            return
         if key not in self.want:
             self.want[key] = spec
             self.dirty = True

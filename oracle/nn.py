@@ -15,7 +15,7 @@ def timestep_embedding(t: torch.Tensor, dim: int, max_period: float = 10000) -> 
     """utils.py:140-158."""
     half = dim // 2
     freqs = torch.exp(-math.log(max_period) * torch.arange(half, dtype=torch.float32) / half)
-    ang = t.reshape(-1, 1).float() * freqs.reshape(1, -1)
+    ang = t.reshape(-1, 1).float() * freqs.reshape(1, -1).to(t.device)
     emb = torch.cat([torch.cos(ang), torch.sin(ang)], dim=1)
     return F.pad(emb, (0, 1)) if dim % 2 else emb
 

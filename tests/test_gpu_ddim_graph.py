@@ -46,3 +46,33 @@ def test_ddim_graph_matches_eager(dims, bf16, monkeypatch):
     for (xa, x0a), (xb, x0b) in zip(traj["0"], traj["1"]):
         assert torch.equal(xa, xb) and torch.equal(x0a, x0b)
     assert not torch.equal(traj["1"][0][1], traj["1"][-1][1])
+
+
+def test_ddim_graph_matches_eager_config2(monkeypatch):
+    """the full-size sampling graph (BASELINE config 2: 128x128x16, joint
+    attention, bf16, the bench's model -- the default sampling path and the bench's DDIM
+    legs) against the eager loop over 3 DDIM steps: the same kernels on the same operands,
+    so bit-equal (this size runs the asm D = 64 / 128 kernels and the D = 256 KV split with
+    its in-capture workspaces, which the 32x32 tests above never reach)."""
+    import argparse
+    import bench
+    from vdiff.engine import sample_ddim, synthetic_clip
+    from vdiff import ops
+    from vdiff.schedulers import DDIMSampler, LinearNoiseSchedulerV2
+    ns = argparse.Namespace(size=128, frames=16, dtype="bf16", mode="joint", init="nonzero")
+    m = bench.build_model(ns, torch.device(dev)).eval()
+    clip = synthetic_clip(1, 16, 128, 500, dev, seed=5)
+    sampler = DDIMSampler(LinearNoiseSchedulerV2(500, 0.00005, 0.015), steps=3)
+    seen = {}
+    with torch.no_grad(), ops.frozen_weights():
+        feats = m.encode_audio(clip.audio)
+        for mode in ("0", "1"):
+            monkeypatch.setenv("VDIFF_DDIM_GRAPH", mode)
+            g = torch.Generator(device=dev).manual_seed(9)
+            seen[mode] = []
+            sample_ddim(m, sampler, clip.cond, feats, tuple(clip.x0.shape), generator=g,
+                        callback=lambda i, xt, x0, s=seen[mode]: s.append(xt.float()))
+    assert len(seen["0"]) == len(seen["1"]) == 3
+    for e, gr in zip(seen["0"], seen["1"]):
+        assert torch.isfinite(e).all() and e.abs().max() > 0
+        assert torch.equal(e, gr), float((gr - e).norm() / e.norm())

@@ -201,7 +201,8 @@ def test_cond_concat_bwd_matches_torch(dtype, hw):
     imc = torch.randn(B, Ci, h, w, generator=g).to(dtype)
     aud = torch.randn(B, T, Ca, generator=g).to(dtype)
     gout = torch.randn((B, 200, T, H, W), generator=g).to(dtype)
-    ir, ar = imc.float().requires_grad_(True), aud.float().requires_grad_(True)
+    ir = imc.float().clone().requires_grad_(True)
+    ar = aud.float().clone().requires_grad_(True)
     ic = F.interpolate(ir, size=(H, W), mode="nearest")[:, :, None].expand(B, Ci, T, H, W)
     au = ar.permute(0, 2, 1)[:, :, :, None, None].expand(B, Ca, T, H, W)
     ref = torch.cat([img.float(), ic, au], 1)

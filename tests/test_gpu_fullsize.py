@@ -171,13 +171,14 @@ def test_attention_full_length(N, C):
     assert eu["o"] < 3e-2 and eu["dq"] < 6e-2 and eu["dk"] < 6e-2 and eu["dv"] < 3e-2, eu
 
 
-def _model(size, frames):
+def _model(size, frames, mode="joint"):
     from vdiff.engine import reinit_nonzero
     from vdiff.unet_audio import UNetAudio
     torch.manual_seed(1234)  # the default (non-zero) layer init draws from the global RNG
     m = UNetAudio(image_size=size, in_channels=3, model_channels=64, out_channels=3,
                   num_res_blocks=2, attention_resolutions=(1, 2, 4), audio_feature_dim=768,
-                  projected_audio_dim=128, dims=3, use_bf16=True, audio_encoder=False)
+                  projected_audio_dim=128, dims=3, use_bf16=True, audio_encoder=False,
+                  attention_mode=mode)
     reinit_nonzero(m, seed=1234)
     return m.to(dev).eval()
 
@@ -202,6 +203,40 @@ def test_config2_model_bf16_vs_fp32():
     e = _rel(y16, y32)
     _record(test="config2_bf16_vs_fp32", rel_l2=e)
     assert e < 3e-2
+
+
+@torch.no_grad()
+def test_config2_model_vs_oracle_spatial_temporal():
+    """the config-2 forward (1x3x16x128x128, the whole audio-conditioned
+    UNet3D) against an INDEPENDENT evaluation -- the oracle's torch restatement
+    (oracle.unet.unet_forward + audio_conditioned_input, pinned to the reference by the
+    golden fixtures) run on the GPU in fp32 with torch's own conv / GroupNorm / softmax --
+    in spatial_temporal mode, the one mode whose reference attention fits: each frame's
+    16384 x 16384 fp32 score matrix is 1 GiB (joint mode would need 275 GB).  Bars: HIP fp32
+    parity mode <= 1e-4 rel-L2, HIP bf16 <= 3e-2 (the survey's bf16 bar)."""
+    from oracle.unet import audio_conditioned_input, build_plan, unet_forward
+    m = _model(128, 16, mode="spatial_temporal")
+    x, cond, feat, t = _model_inputs(128, 16, 11)
+    y16 = m(x, cond, feat, t).float()
+    m.convert_to_fp32()
+    y32 = m(x, cond, feat, t).float()
+    P = {k: v.detach().float() for k, v in m.state_dict().items()}
+    plan = build_plan(in_channels=195, model_channels=64, out_channels=3, num_res_blocks=2,
+                      attention_resolutions=(1, 2, 4), channel_mult=(1, 2, 4), dims=3,
+                      attention_mode="spatial_temporal")
+    del m
+    torch.cuda.empty_cache()
+    prev = torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
+    try:
+        yr = unet_forward(P, plan, audio_conditioned_input(P, x, cond, feat, 128), t).float()
+    finally:
+        torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = prev
+    assert torch.isfinite(yr).all() and yr.abs().max() > 0
+    e32, e16 = _rel(y32, yr), _rel(y16, yr)
+    _record(test="config2_spatial_temporal_vs_oracle", rel_l2_fp32=e32, rel_l2_bf16=e16)
+    assert e32 < 1e-4, e32
+    assert e16 < 3e-2, e16
 
 
 @torch.no_grad()

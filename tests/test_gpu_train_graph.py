@@ -14,6 +14,12 @@ dev = "cuda"
 GOLDEN = 0x9E3779B97F4A7C15
 
 
+@pytest.fixture(autouse=True)
+def _experimental(monkeypatch):
+    """Trainer(graph=True) is gated behind VDIFF_TRAIN_GRAPH_EXPERIMENTAL (advisor r03)."""
+    monkeypatch.setenv("VDIFF_TRAIN_GRAPH_EXPERIMENTAL", "1")
+
+
 def _tiny_w2v(hidden=64):
     """A one-layer wav2vec2 with every stochastic part off (dropouts, LayerDrop, SpecAugment),
     so the eager and the graph runs see the same encoder computation."""

@@ -93,3 +93,11 @@ def test_ddp_nonfinite_loss_raises_on_every_rank():
         p.join(timeout=60)
     for r in (0, 1):
         assert got[r].startswith("raised after 4 steps") and "step 2 " in got[r], got
+
+
+def test_graph_trainer_is_gated(monkeypatch):
+    """Advisor r03: Trainer(graph=True) (replays with a known defect at the config-2 scale)
+    raises unless VDIFF_TRAIN_GRAPH_EXPERIMENTAL=1 opts in."""
+    monkeypatch.delenv("VDIFF_TRAIN_GRAPH_EXPERIMENTAL", raising=False)
+    with pytest.raises(RuntimeError, match="VDIFF_TRAIN_GRAPH_EXPERIMENTAL"):
+        Trainer(_Model(set()), _Sched(), lr=1e-3, graph=True)

@@ -62,9 +62,12 @@ void fill_guard(char* p) {
 
 // check the given blocks (the `bytes` of each guard nearest the user region); returns the
 // number of corrupt guards and prints them
+std::mutex g_check_mu;  // check_blocks' persistent device arrays
+
 int check_blocks(const std::vector<std::pair<void*, Blk>>& blks, const char* when,
                  size_t bytes = kGuard) {
   if (blks.empty()) return 0;
+  std::lock_guard<std::mutex> lk(g_check_mu);
   if (bytes > kGuard) bytes = kGuard;
   const int n = (int)blks.size() * 2;
   std::vector<const uint32_t*> gp(n);
@@ -73,18 +76,26 @@ int check_blocks(const std::vector<std::pair<void*, Blk>>& blks, const char* whe
     gp[2 * i] = reinterpret_cast<const uint32_t*>(b.base + kGuard - bytes);
     gp[2 * i + 1] = reinterpret_cast<const uint32_t*>(b.base + kGuard + b.size);
   }
-  const uint32_t** dg = nullptr;
-  long long* dbad = nullptr;
-  if (hipMalloc(&dg, n * sizeof(void*)) || hipMalloc(&dbad, n * sizeof(long long))) {
-    fprintf(stderr, "[guard] hipMalloc failed in check\n");
-    return -1;
+  // persistent device arrays for the guard pointers and results (grown, never freed)
+  static const uint32_t** dg = nullptr;
+  static long long* dbad = nullptr;
+  static int cap = 0;
+  if (n > cap) {
+    if (dg) (void)hipFree(dg);
+    if (dbad) (void)hipFree(dbad);
+    cap = n * 2 + 1024;
+    if (hipMalloc(&dg, cap * sizeof(void*)) || hipMalloc(&dbad, cap * sizeof(long long))) {
+      fprintf(stderr, "[guard] hipMalloc failed in check\n");
+      cap = 0;
+      dg = nullptr;
+      dbad = nullptr;
+      return -1;
+    }
   }
   (void)hipMemcpy(dg, gp.data(), n * sizeof(void*), hipMemcpyHostToDevice);
   check_kernel<<<n, 256>>>(dg, n, bytes / 4, dbad);
   std::vector<long long> bad(n);
   (void)hipMemcpy(bad.data(), dbad, n * sizeof(long long), hipMemcpyDeviceToHost);
-  (void)hipFree(dg);
-  (void)hipFree(dbad);
   int nbad = 0;
   for (int i = 0; i < n; ++i) {
     // atomicMin on -1 (as unsigned: max) keeps -1 when clean
