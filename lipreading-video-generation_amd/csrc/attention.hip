@@ -1870,6 +1870,12 @@ int cfg_from_env() {
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
 
+// D = 256 hand-scheduled dQ as the default: off until measured on the GPU (VDIFF_ASM256=1)
+const bool g_asm256 = [] {
+  const char* e = getenv("VDIFF_ASM256");
+  return e && atoi(e) == 1;
+}();
+
 AttnCfg pick_cfg(int D, bool bf16, int kind) {
   const int env = g_cfg.load(std::memory_order_relaxed);
   if (!bf16) return kBase;
@@ -1890,12 +1896,12 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
       !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
-      !(env == kAsm && D != 64 && D != 128) &&       // hand-scheduled: D = 64, 128
+      !(env == kAsm && D != 64 && D != 128 && !(D == 256 && kind != 0)) &&  // hand-scheduled
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kAsm;  // falls back to D8N / P8 off its shapes
   else if (D == 128) c = kAsm;  // asm falls back to D8N / W8 / PAIR off its shapes
-  else if (D == 256 && kind == 2) c = kRole;
+  else if (D == 256 && kind != 0) c = g_asm256 ? kAsm : (kind == 2 ? kRole : kBase);
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
   if (c == kP8 && D != 64) c = kP4;
@@ -1948,6 +1954,36 @@ int role_q_splits(const vd_attn_desc* d, int nkv) {
   return s;
 }
 
+// key splits (log2) of the hand-scheduled head_dim-256 dQ: the query grid (128 queries per
+// workgroup) times the splits covers the 256 CUs, at most 4 splits, every split non-empty
+// and a whole number of 4-tile (128-key) loop iterations
+int dq256_lsplit(const vd_attn_desc* d) {
+  const int64_t n = d->seq_len, wgs = vd_cdiv(n, 128) * d->nseq;
+  int l = 0;
+  while (l < 2 && (wgs << l) < 256) {
+    const int64_t S = 2 << l, kps = vd_cdiv(vd_cdiv(n, S), 128) * 128;
+    if ((S - 1) * kps >= n) break;
+    ++l;
+  }
+  return l;
+}
+int64_t dq256_kps(const vd_attn_desc* d, int l) {
+  return vd_cdiv(vd_cdiv(d->seq_len, (int64_t)1 << l), 128) * 128;
+}
+
+// query splits (log2) of the hand-scheduled head_dim-256 dK/dV (64 keys per workgroup): up to
+// 16, every split non-empty and a whole number of 4-tile (128-query) loop iterations
+int dkdv256_lsplit(const vd_attn_desc* d) {
+  const int64_t n = d->seq_len, wgs = vd_cdiv(n, 64) * d->nseq;
+  int l = 0;
+  while (l < 4 && (wgs << l) < 256) {
+    const int64_t S = 2 << l, qps = vd_cdiv(vd_cdiv(n, S), 128) * 128;
+    if ((S - 1) * qps >= n) break;
+    ++l;
+  }
+  return l;
+}
+
 // Backward workspace: [ndelta rows][nlse2 rows][64 floats][dQ KV-split partials]
 // [dK/dV query-split partials]; rows = nseq * seq_len (queries).
 struct BwdWs {
@@ -1960,9 +1996,15 @@ BwdWs bwd_ws(const vd_attn_desc* d, int nkv, bool cross) {
   const size_t rows = (size_t)d->nseq * d->seq_len;
   if (d->dtype == VD_BF16 && (cross || pick_cfg(D, true, 1) == kBase))
     w.sdq = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv);
+  // hand-scheduled D = 256 dQ: its key splits (the compiled fallback of a misaligned call
+  // splits as the base shape does; the partial region fits either)
+  if (D == 256 && !cross && d->dtype == VD_BF16 && pick_cfg(D, true, 1) == kAsm)
+    w.sdq = std::max(1 << dq256_lsplit(d), kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv));
   if (cross || (d->dtype == VD_BF16 && pick_cfg(D, true, 2) == kBase)) w.sq = q_splits<D>(d, nkv);
   else if (D == 256 && d->dtype == VD_BF16 && pick_cfg(D, true, 2) == kRole)
     w.sq = role_q_splits(d, nkv);
+  else if (D == 256 && d->dtype == VD_BF16 && pick_cfg(D, true, 2) == kAsm)
+    w.sq = std::max(1 << dkdv256_lsplit(d), q_splits<D>(d, nkv));  // (+ the base fallback)
   w.dq_off = 2 * rows + 64;
   w.kv_off = w.dq_off + (w.sdq > 1 ? (size_t)w.sdq * rows * D : 0);
   const size_t kvp = w.sq > 1 ? (size_t)w.sq * d->nseq * nkv * 2 * D : 0;
@@ -2184,6 +2226,100 @@ int dq_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const voi
   return rc ? rc : vd::check_launch("attn_bwd_dq");
 }
 
+// hand-scheduled head_dim-256 dQ (asm/gen_d256.py, 128 queries per workgroup) with its key
+// split into fp32 partials (part: the dQ partial region of the backward workspace)
+int dq256_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                     const void* dout, const float* nlse2, const float* ndelta, void* dq,
+                     float* part, hipStream_t st) {
+  const int64_t n = d->seq_len;
+  const int l = dq256_lsplit(d);
+  const int64_t kps = dq256_kps(d, l);
+  vd::AsmDq256Args a{};
+  vd::AsmDqArgs& b = a.b;
+  b.q = q; b.k = k; b.v = v; b.dout = dout; b.nlse2 = nlse2; b.ndelta = ndelta; b.dq = dq;
+  b.n = (uint32_t)n;
+  b.ts_bytes = (uint32_t)(d->token_stride * 2);
+  b.ots_bytes = (uint32_t)(d->o_token_stride * 2);
+  b.groups = (uint32_t)d->groups;
+  b.bs_bytes = (uint64_t)d->batch_stride * 2;
+  b.gs_bytes = (uint64_t)d->group_stride * 2;
+  b.obs_bytes = (uint64_t)d->o_batch_stride * 2;
+  b.ogs_bytes = (uint64_t)d->o_group_stride * 2;
+  b.scale = d->scale;
+  b.qscale = d->scale * kLog2e;
+  b.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 256) * 2);
+  b.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 256) * 2);
+  b.tile_bytes = (uint32_t)(32 * d->token_stride * 2);
+  b.niter = (uint32_t)vd_cdiv(vd_cdiv(kps, 32), 4);
+  a.part = l ? part : nullptr;
+  a.kps = (uint32_t)kps;
+  a.lsplit = (uint32_t)l;
+  a.split_bytes = (uint64_t)d->nseq * n * 1024;
+  a.part_bytes = (uint32_t)(n * 1024);
+  const unsigned gy = (unsigned)d->groups, gz = (unsigned)(d->nseq / d->groups) << l;
+  int rc = vd::asm_bwd_dq_d256(a, (unsigned)vd_cdiv(n, 128), gy, gz, st);
+  if (rc) return rc;
+  if (l) {
+    rc = vd::check_launch("attn_bwd_dq");
+    if (rc) return rc;
+    const SeqAddr qa{d->batch_stride, d->group_stride, d->groups};
+    const int64_t work = (int64_t)d->nseq * n * (256 / 8);
+    int g = (int)vd_cdiv(work, 256);
+    if (g > 4096) g = 4096;
+    attn_dq_sum_kernel<bf16_t, 256><<<g, 256, 0, st>>>(part, 1 << l, d->nseq, (int)n,
+                                                       (bf16_t*)dq, qa, d->token_stride);
+  }
+  return vd::check_launch("attn_bwd_dq");
+}
+
+// hand-scheduled head_dim-256 dK/dV (asm/gen_d256dk.py, role-split wave pairs, 64 keys per
+// workgroup) with its query split into fp32 partials (part: the dK/dV partial region)
+int dkdv256_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                       const void* dout, const float* nlse2, const float* ndelta, void* dk,
+                       void* dv, float* part, hipStream_t st) {
+  const int64_t n = d->seq_len;
+  const int l = dkdv256_lsplit(d);
+  const int64_t qps = vd_cdiv(vd_cdiv(n, (int64_t)1 << l), 128) * 128;
+  vd::AsmDkdv256Args a{};
+  vd::AsmDkdvArgs& b = a.b;
+  b.q = q; b.k = k; b.v = v; b.dout = dout; b.nlse2 = nlse2; b.ndelta = ndelta;
+  b.dk = dk; b.dv = dv;
+  b.n = (uint32_t)n;
+  b.ts_bytes = (uint32_t)(d->token_stride * 2);
+  b.ots_bytes = (uint32_t)(d->o_token_stride * 2);
+  b.groups = (uint32_t)d->groups;
+  b.bs_bytes = (uint64_t)d->batch_stride * 2;
+  b.gs_bytes = (uint64_t)d->group_stride * 2;
+  b.obs_bytes = (uint64_t)d->o_batch_stride * 2;
+  b.ogs_bytes = (uint64_t)d->o_group_stride * 2;
+  b.scale = d->scale;
+  b.kscale = d->scale * kLog2e;
+  b.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 256) * 2);
+  b.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 256) * 2);
+  b.tile_bytes = (uint32_t)(32 * d->token_stride * 2);
+  b.otile_bytes = (uint32_t)(32 * d->o_token_stride * 2);
+  b.niter = (uint32_t)vd_cdiv(vd_cdiv(qps, 32), 4);
+  a.part = l ? part : nullptr;
+  a.qps = (uint32_t)qps;
+  a.lsplit = (uint32_t)l;
+  a.split_bytes = (uint64_t)d->nseq * n * 2048;
+  a.part_bytes = (uint32_t)(n * 2048);
+  const unsigned gy = (unsigned)d->groups, gz = (unsigned)(d->nseq / d->groups) << l;
+  int rc = vd::asm_bwd_dkdv_d256(a, (unsigned)vd_cdiv(n, 64), gy, gz, st);
+  if (rc) return rc;
+  if (l) {
+    rc = vd::check_launch("attn_bwd_dkdv");
+    if (rc) return rc;
+    const int64_t work = (int64_t)d->nseq * n * (2 * 256 / 8);
+    int g = (int)vd_cdiv(work, 256);
+    if (g > 4096) g = 4096;
+    attn_dkdv_sum_kernel<bf16_t, 256><<<g, 256, 0, st>>>(part, 1 << l, d->nseq, (int)n,
+                                                         (bf16_t*)dk, (bf16_t*)dv,
+                                                         self_kv(d).a, d->token_stride);
+  }
+  return vd::check_launch("attn_bwd_dkdv");
+}
+
 // hand-scheduled dK/dV: head_dim 64 (256 keys per workgroup) or 128 (asm/gen_d128.py, 128)
 int dkdv_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                     const void* dout, const float* nlse2, const float* ndelta, void* dk, void* dv,
@@ -2248,6 +2384,12 @@ int bwd_dq_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, con
       if (c == kP4N2) return dq_pipe_launch<T, D, 4, 2>(d, q, k, v, dout, nlse2, ndelta, dq, st);
     if constexpr (D <= 128)
       if (c == kP4) return dq_pipe_launch<T, D, 4>(d, q, k, v, dout, nlse2, ndelta, dq, st);
+    if constexpr (D == 256)
+      if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dq, D)) {
+        const BwdWs w = bwd_ws<D>(d, kv.n, cross);
+        return dq256_asm_launch(d, q, k, v, dout, nlse2, ndelta, dq,
+                                reinterpret_cast<float*>(ws) + w.dq_off, st);
+      }
   }
   // the 4-wave, 32-row shape splits the keys when its grid leaves CUs idle (bf16, D = 256):
   // fp32 partials after the row constants in the workspace (vd_attention_bwd_workspace_size)
@@ -2384,6 +2526,12 @@ int bwd_dkdv_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, c
     if constexpr (D == 128)
       if (c == kPair || c == kAsm)
         return dkdv_pair_launch<D>(d, kv, q, k, v, dout, nlse2, ndelta, dk, dv, st);
+    if constexpr (D == 256)
+      if (c == kAsm && asm_dq_ok(d, q, k, v, dout, dk, D) && asm_dq_ok(d, q, k, v, dout, dv, D)) {
+        const BwdWs w = bwd_ws<D>(d, kv.n, cross);
+        return dkdv256_asm_launch(d, q, k, v, dout, nlse2, ndelta, dk, dv,
+                                  reinterpret_cast<float*>(ws) + w.kv_off, st);
+      }
     if constexpr (D == 256)
       if (c == kRole) {
         const BwdWs w = bwd_ws<D>(d, kv.n, cross);

@@ -81,4 +81,35 @@ int asm_fwd_d64(const AsmFwdArgs& a, unsigned gx, unsigned gy, unsigned gz, hipS
 // = 256-key iterations, klim0); grid (ceil(n / 256), groups, nseq / groups), 128 KiB LDS
 int asm_fwd_d128(const AsmFwdArgs& a, unsigned gx, unsigned gy, unsigned gz, hipStream_t stream);
 
+// vd_attn_bwd_dq_d256 (asm/gen_d256.py): the dQ block plus the key split -- split z of
+// 2^lsplit takes keys [z kps, (z + 1) kps) and, with part != 0, writes dQ * scale as fp32
+// partials part[z][seq][n][256] (split_bytes = nseq * n * 1024, part_bytes = n * 1024).
+// grid (ceil(n / 128), groups, (nseq / groups) << lsplit), 256 threads, 128 KiB static LDS
+struct AsmDq256Args {
+  AsmDqArgs b;
+  float* part;
+  uint32_t kps, lsplit;
+  uint64_t split_bytes;
+  uint32_t part_bytes, pad;
+};
+static_assert(sizeof(AsmDq256Args) == 160, "kernarg block layout");
+int asm_bwd_dq_d256(const AsmDq256Args& a, unsigned gx, unsigned gy, unsigned gz,
+                    hipStream_t stream);
+
+// vd_attn_bwd_dkdv_d256 (asm/gen_d256dk.py): the dK/dV block plus the query split -- split z
+// of 2^lsplit takes queries [z qps, (z + 1) qps) and, with part != 0, writes fp32 partials
+// part[z][seq][nkv][dK 256 | dV 256] (dK times scale; split_bytes = nseq * nkv * 2048,
+// part_bytes = nkv * 2048).  tile_bytes / otile_bytes: 32 rows of q / dout.
+// grid (ceil(n / 64), groups, (nseq / groups) << lsplit), 256 threads, 147 KiB static LDS
+struct AsmDkdv256Args {
+  AsmDkdvArgs b;
+  float* part;
+  uint32_t qps, lsplit;
+  uint64_t split_bytes;
+  uint32_t part_bytes, pad;
+};
+static_assert(sizeof(AsmDkdv256Args) == 176, "kernarg block layout");
+int asm_bwd_dkdv_d256(const AsmDkdv256Args& a, unsigned gx, unsigned gy, unsigned gz,
+                      hipStream_t stream);
+
 }  // namespace vd

@@ -23,7 +23,9 @@ def gens():
         import gen_d128 as D128
         import gen_fwd as F64
         import gen_fwd128 as F128
-        yield G, F64, D128, F128
+        import gen_d256 as D256
+        import gen_d256dk as D256K
+        yield G, F64, D128, F128, D256, D256K
     finally:
         sys.path.remove(ASM)
 
@@ -35,15 +37,17 @@ def test_code_object_assembles(tmp_path, gens):
     subprocess.run([sys.executable, os.path.join(ASM, "gen_attn_asm.py"), str(out)], check=True)
     text = out.read_text()
     for name in ("vd_attn_bwd_dq_d64", "vd_attn_bwd_dkdv_d64", "vd_attn_fwd_d64",
-                 "vd_attn_bwd_dkdv_d128", "vd_attn_bwd_dq_d128", "vd_attn_fwd_d128"):
+                 "vd_attn_bwd_dkdv_d128", "vd_attn_bwd_dq_d128", "vd_attn_fwd_d128",
+                 "vd_attn_bwd_dq_d256", "vd_attn_bwd_dkdv_d256"):
         assert f".amdhsa_kernel {name}" in text, name
     subprocess.run([CLANG, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
                     "-c", str(out), "-o", str(tmp_path / "a.o")], check=True)
 
 
 def test_register_budgets(gens):
-    G, F64, D128, F128 = gens
-    for regs in (G.regs_dq, G.regs_dkdv, F64.regs, D128.regs, D128.dq_regs, F128.regs):
+    G, F64, D128, F128, D256, D256K = gens
+    for regs in (G.regs_dq, G.regs_dkdv, F64.regs, D128.regs, D128.dq_regs, F128.regs,
+                 D256.regs, D256K.regs_a, D256K.regs_b):
         V, A = regs()
         assert V.next <= 256 and A.next <= 256, (regs, V.next, A.next)
         assert (V.next + 3) // 4 * 4 + A.next <= 512
@@ -57,7 +61,7 @@ def _body_counts(lines, start, stop):
 
 
 def test_instruction_mix_per_tile(gens):
-    G, F64, D128, F128 = gens
+    G, F64, D128, F128, D256, D256K = gens
     mf = "v_mfma_f32_32x32x16_bf16"
     _, _, st = D128.gen_dkdv128()
     c = _body_counts(st.lines, "query tile, ring stage 1", "query tile, ring stage 2")
@@ -74,3 +78,39 @@ def test_instruction_mix_per_tile(gens):
     c = _body_counts(st.lines, "body, stage 1", "body, stage 2")
     assert c[mf] == 32 and c["v_exp_f32"] == 64 and c["v_cvt_pk_bf16_f32"] == 32
     assert c.get("s_nop", 0) <= 8
+    # head_dim 256 (round 4): dQ 48 MFMAs per 32-key tile, 8 + 8 row / 32 transposed reads
+    _, _, st = D256.gen_dq256()
+    c = _body_counts(st.lines, "key tile, ring stage 1", "key tile, ring stage 2")
+    assert c[mf] == 48 and c["v_exp_f32"] == 16 and c["v_cvt_pk_bf16_f32"] == 8
+    assert c["ds_read_b128"] == 32 and c["ds_read_b64_tr_b16"] == 32
+    assert c["buffer_load_dwordx4"] == 8 and c.get("s_nop", 0) <= 16
+    # dK / dV role pairs: 32 MFMAs per 32-query tile in each role, 9 DMA ops
+    _, _, st = D256K.gen_dkdv256()
+    c = _body_counts(st.lines, "A: query tile, ring stage 1", "A: query tile, ring stage 2")
+    assert c[mf] == 32 and c["v_exp_f32"] == 16 and c["ds_write_b128"] == 4
+    assert c["buffer_load_dwordx4"] == 8 and c["buffer_load_dword"] == 1
+    assert c.get("s_nop", 0) <= 20
+    c = _body_counts(st.lines, "B: query tile, ring stage 1", "B: query tile, ring stage 2")
+    assert c[mf] == 32 and c["v_mul_f32"] == 16 and c["ds_read_b128"] == 16 + 4 + 4
+    assert c.get("s_nop", 0) <= 20
+
+
+def test_d256_lane_tables(gens):
+    """The head_dim-256 lane tables: 32 u32 per lane, the DMA pieces of the 4 waves (dQ) /
+    2 pairs (dK/dV) cover every (row, 16-B chunk) of a 32-row tile exactly once."""
+    G, F64, D128, F128, D256, D256K = gens
+    t = D256.lane_table()
+    assert len(t) == 256 and all(len(r) == 32 for r in t)
+    seen = set()
+    for w in range(4):
+        for lane in range(64):
+            for i in range(4):
+                seen.add((t[64 * w + lane][16 + i], t[64 * w + lane][20 + i]))
+    assert len(seen) == 32 * 32
+    t = D256K.lane_table()
+    seen = set()
+    for w in range(2):  # pair 0 / 1 (waves 2, 3 repeat them for the dO tile)
+        for lane in range(64):
+            for i in range(8):
+                seen.add((t[64 * w + lane][16 + i], t[64 * w + lane][24 + i]))
+    assert len(seen) == 32 * 32

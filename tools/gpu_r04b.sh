@@ -44,3 +44,5 @@ done
 PMC_OUT=gpurun_out/${T}_pmc256 timeout -k 10 900 bash tools/pmc_attn.sh --only 256 \
   > gpurun_out/${T}_pmc256.log 2>&1 || { echo "pmc rc=$?"; tail -5 gpurun_out/${T}_pmc256.log; exit 1; }
 cat gpurun_out/${T}_pmc256/pmc_attn.md
+# (6) the hand-scheduled head_dim-256 backward kernels (new; last, each step time-limited)
+bash tools/gpu_r04c.sh ${T}c
