@@ -12,7 +12,7 @@ module provides
   * `kernel_text` -- the code object wrapper (.amdhsa_kernel descriptor + metadata).
 
 Hazard distances (gfx950, measured from hipcc's own padding of the same instruction pairs):
-MFMA 32x32x16 write -> VALU / VMEM / DS / MFMA-A/B read 12 wait states; VALU write -> MFMA
+MFMA 32x32x16 write -> VALU / VMEM / DS / MFMA-A/B read 12 wait states (16x16x32: 8); VALU write -> MFMA
 read 2; transcendental write -> VALU read 2 (one instruction between); an MFMA reading its
 own accumulator chain as srcC needs none.  Wait states are counted as issued instructions
 (s_nop n = n + 1), which under-counts the cycles an MFMA occupies, so the padding is
@@ -120,6 +120,7 @@ class Stream:
     explicit lgkmcnt(0))."""
 
     MFMA_RAW = 12      # MFMA write -> VALU / VMEM / DS / MFMA A-B read (and write)
+    MFMA16_RAW = 8     # ... of a 16x16 (4-pass) MFMA (hipcc: s_nop 7 before the VALU read)
     VALU_TO_MFMA = 2   # VALU write -> MFMA read
     TRANS_RAW = 2      # transcendental write -> VALU read
     MFMA_WAR = 12      # VALU write of an in-flight MFMA's source
@@ -154,13 +155,14 @@ class Stream:
             if d >= 13:
                 break
             if h.kind == "mfma":
+                raw = self.MFMA16_RAW if "_16x16x" in h.op else self.MFMA_RAW
                 if ins.kind == "mfma":
                     # chained accumulator (srcC == the producer's dst) needs no padding
                     touched = (ins.uses - ins.srcc) & h.defs
                     if touched:
-                        need = max(need, self.MFMA_RAW - d)
+                        need = max(need, raw - d)
                 elif (ins.uses | ins.defs) & h.defs:
-                    need = max(need, self.MFMA_RAW - d)
+                    need = max(need, raw - d)
                 if ins.kind in ("valu", "trans", "ds", "vmem") and ins.defs & (h.uses | h.srcc):
                     need = max(need, self.MFMA_WAR - d)
             elif h.kind in ("valu", "trans"):

@@ -51,7 +51,9 @@ LAG1 = 0               # CHAINS = 1 through the lagged list (adds 4 scores behin
 DMAS = 0               # LDS-DMA slots of a body: 0 {4,12,20,28} 1 {1,9,17,25} 2 {6,14,22,30}
                        # 3 {0,8,16,24}
 MSUM = 0               # row sums on the matrix pipe: 8 MFMAs (ones x P^T) per body replace the
-                       # 64 v_add_f32; the tile's lagged-max check moves to the next body's top
+                       # 64 v_add_f32; the tile's lagged-max check moves to the next body's top.
+                       # 1: 32x32x16 (ones x P^T); 2: 16x16x32 with a lane-group selector as
+                       # the A operand (half the matrix-pipe time, both lane halves summed)
 
 # kernel arguments (AsmFwdArgs in vd_asm.h), loaded into s[16:43]:
 #  0 q  8 k  16 v  24 o  32 lse                            (u64)   s16..s25
@@ -80,7 +82,10 @@ def regs():
     A.alloc("acc", 64)       # O^T accumulators [i][j]
     A.alloc("kf", 32)        # K row fragments [kb][s]
     A.alloc("trf", 32)       # V^T fragments [kb][i][s2] (lo 2 + hi 2)
-    if MSUM:
+    if MSUM == 2:
+        A.alloc("lsum", 8)   # tile row sums [j] (all 4 rows of a lane hold its query's sum)
+        A.alloc("sel", 4)    # bf16 lane-group selector A operand (sum16_mfmas)
+    elif MSUM:
         A.alloc("lsum", 32)  # tile row sums [j] (all 16 rows of a block hold the lane's sum)
         A.alloc("ones", 4)   # bf16 1.0 A operand
     return V, A
@@ -138,6 +143,23 @@ def sum_mfmas(V, A):
         for n, (kb, s2) in enumerate((kb, s2) for kb in range(2) for s2 in range(2)):
             c = "0" if n == 0 else acc
             out.append((f"{MFMA} {acc}, {A.r('ones', 0, 4)}, "
+                        f"{V.r('p', 8 * (2 * kb + j) + 4 * s2, 4)}, {c}", ()))
+    return out
+
+
+def sum16_mfmas(V, A):
+    """MSUM 2: lsum[j] = the tile's row sums of P^T (bf16) by v_mfma_f32_16x16x32_bf16.  The
+    B operand of lane l = 16 g + n is its P^T quad: 8 keys of query 16 (g & 1) + n, key half
+    g >> 1.  The A operand `sel` of lane 16 g + m is 1.0 where (g & 1) == ((m >> 2) & 1), so
+    D row m (held by lane group m >> 2) sums the lane groups of the same query parity: every
+    lane's 4 result rows are its own query's sum over both key halves of the 16-key chunk.
+    The k order within a lane group does not matter (A and B lanes cover the same k)."""
+    out = []
+    for n, (kb, s2) in enumerate((kb, s2) for kb in range(2) for s2 in range(2)):
+        for j in range(2):
+            acc = A.r("lsum", 4 * j, 4)
+            c = "0" if n == 0 else acc
+            out.append((f"v_mfma_f32_16x16x32_bf16 {acc}, {A.r('sel', 0, 4)}, "
                         f"{V.r('p', 8 * (2 * kb + j) + 4 * s2, 4)}, {c}", ()))
     return out
 
@@ -409,7 +431,20 @@ def prologue(st: Stream, V, A):
         e(f"v_mov_b32 {V.r('l', j)}, 0")
         e(f"v_mov_b32 {V.r('ps', j)}, 0")
     e(f"v_mov_b32 {V.r('ninf')}, {NINF}")
-    if MSUM:  # the "tile -1" check of the first body passes (sum 0)
+    if MSUM == 2:  # sel (sum16_mfmas); the "tile -1" check of the first body passes (sum 0)
+        t0, t1 = V.r("tmp", 0), V.r("tmp", 1)
+        e(f"v_lshrrev_b32 {t0}, 2, {V.r('lane')}")
+        e(f"v_lshrrev_b32 {t1}, 4, {V.r('lane')}")
+        e(f"v_xor_b32 {t0}, {t0}, {t1}")
+        e(f"v_and_b32 {t0}, 1, {t0}")
+        e(f"v_cmp_eq_u32 vcc, 0, {t0}")
+        e(f"v_mov_b32 {t1}, 0x3f803f80")
+        e(f"v_cndmask_b32 {t0}, 0, {t1}, vcc")
+        for k in range(4):
+            e(f"v_accvgpr_write_b32 {A.r('sel', k)}, {t0}")
+        for k in range(8):
+            e(f"v_accvgpr_write_b32 {A.r('lsum', k)}, 0")
+    elif MSUM:  # the "tile -1" check of the first body passes (sum 0)
         e(f"v_mov_b32 {V.r('tmp', 0)}, 0x3f803f80")
         for k in range(4):
             e(f"v_accvgpr_write_b32 {A.r('ones', k)}, {V.r('tmp', 0)}")
@@ -450,7 +485,7 @@ def emit_check(st: Stream, V, A, u, masked, tag, msum):
     tc = V.r("tc", 0)
     if msum:
         for j in range(2):
-            st.emit(f"v_accvgpr_read_b32 {V.r('ps', j)}, {A.r('lsum', 16 * j)}")
+            st.emit(f"v_accvgpr_read_b32 {V.r('ps', j)}, {A.r('lsum', (4 if MSUM == 2 else 16) * j)}")
     st.emit(f"v_max_f32 {tc}, {V.r('ps', 0)}, {V.r('ps', 1)}")
     st.emit(f"v_cmp_ngt_f32 vcc, 0x47800000, {tc}")
     if CHECK_NOP:
@@ -540,8 +575,16 @@ def emit_body_msum(st: Stream, V, A, u, masked, tag, prev):
         if u == 0 and not masked:
             st.raw("s_nop 7")  # the loop back edge: SUM(t-1) of the last body wrote lsum
         emit_check(st, V, A, prev[0], prev[1], f"c{tag}", True)
-    mf = (g_mfmas(V, A, 0) + g_mfmas(V, A, 1) + s_mfmas(V, A, 1 - par, 0) + sum_mfmas(V, A)
-          + s_mfmas(V, A, 1 - par, 1))
+    if MSUM == 2:
+        # G(t-1) kb0 | G(t-1) kb1 | S(t+1) kb0 | S(t+1) kb1 | SUM(t) (8 x 16x16x32); the
+        # softmax over gaps 0..31 as in the adds body
+        mf = (g_mfmas(V, A, 0) + g_mfmas(V, A, 1) + s_mfmas(V, A, 1 - par, 0)
+              + s_mfmas(V, A, 1 - par, 1) + sum16_mfmas(V, A))
+        rslots, dma_at, ngap = (2, 8, 12, 16), {4: 0, 12: 1, 20: 2, 28: 3}, 32
+    else:
+        mf = (g_mfmas(V, A, 0) + g_mfmas(V, A, 1) + s_mfmas(V, A, 1 - par, 0)
+              + sum_mfmas(V, A) + s_mfmas(V, A, 1 - par, 1))
+        rslots, dma_at, ngap = (2, 24, 12, 32), {4: 0, 12: 1, 34: 2, 38: 3}, 24
     nm = len(mf)
     reads = {}
 
@@ -551,13 +594,12 @@ def emit_body_msum(st: Stream, V, A, u, masked, tag, prev):
 
     kst = (u + 1) % NST
     if not DROP & 8:
-        put(2, k_reads(V, A, kst, 0))   # K(t+1) rows kb0 (S kb0 at 16..23)
-        put(12, k_reads(V, A, kst, 1))  # kb1 (S kb1 at 32..39)
-        put(24, tr_reads(V, A, u, 0))   # V(t)^T for G(t) in the next body
-        put(32, tr_reads(V, A, u, 1))
+        put(rslots[0], k_reads(V, A, kst, 0))   # K(t+1) rows kb0
+        put(rslots[2], k_reads(V, A, kst, 1))   # kb1
+        put(rslots[1], tr_reads(V, A, u, 0))    # V(t)^T for G(t) in the next body
+        put(rslots[3], tr_reads(V, A, u, 1))
     ops, adv = dma_ops(V, (u + PD) % NST)
-    dma_at = {4: 0, 12: 1, 34: 2, 38: 3}
-    valu = place(softmax_list(V, par, masked, u), 24)
+    valu = place(softmax_list(V, par, masked, u), ngap)
     for g in range(nm):
         if g in dma_at:
             m0, ld = ops[dma_at[g]]
@@ -569,7 +611,7 @@ def emit_body_msum(st: Stream, V, A, u, masked, tag, prev):
                     st.emit(a)
         for text, rid in reads.get(g, []):
             st.emit(text, lds_id=rid)
-        if g < 24:
+        if g < ngap:
             for text in valu[g]:
                 st.emit(text)
         text, deps = mf[g]

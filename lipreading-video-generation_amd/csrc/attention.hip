@@ -1957,10 +1957,16 @@ int role_q_splits(const vd_attn_desc* d, int nkv) {
 // key splits (log2) of the hand-scheduled head_dim-256 dQ: the query grid (128 queries per
 // workgroup) times the splits covers the 256 CUs, at most 4 splits, every split non-empty
 // and a whole number of 4-tile (128-key) loop iterations
+// VDIFF_ASM256_DQ_L / VDIFF_ASM256_DKDV_L (diagnostics): cap the split count's log2
+static int lsplit_cap(const char* env, int dflt) {
+  const char* e = getenv(env);
+  return e ? std::max(0, std::min(dflt, atoi(e))) : dflt;
+}
 int dq256_lsplit(const vd_attn_desc* d) {
   const int64_t n = d->seq_len, wgs = vd_cdiv(n, 128) * d->nseq;
+  const int cap = lsplit_cap("VDIFF_ASM256_DQ_L", 2);
   int l = 0;
-  while (l < 2 && (wgs << l) < 256) {
+  while (l < cap && (wgs << l) < 256) {
     const int64_t S = 2 << l, kps = vd_cdiv(vd_cdiv(n, S), 128) * 128;
     if ((S - 1) * kps >= n) break;
     ++l;
@@ -1975,8 +1981,9 @@ int64_t dq256_kps(const vd_attn_desc* d, int l) {
 // 16, every split non-empty and a whole number of 4-tile (128-query) loop iterations
 int dkdv256_lsplit(const vd_attn_desc* d) {
   const int64_t n = d->seq_len, wgs = vd_cdiv(n, 64) * d->nseq;
+  const int cap = lsplit_cap("VDIFF_ASM256_DKDV_L", 4);
   int l = 0;
-  while (l < 4 && (wgs << l) < 256) {
+  while (l < cap && (wgs << l) < 256) {
     const int64_t S = 2 << l, qps = vd_cdiv(vd_cdiv(n, S), 128) * 128;
     if ((S - 1) * qps >= n) break;
     ++l;

@@ -5,7 +5,12 @@ weights never move and every step sees the same operands.  With every reduction 
 (round 4), each replay must equal the eager step BIT FOR BIT: loss and every parameter
 gradient.  Prints, per step, the loss pair and the parameters whose gradients differ
 (backward order: the first listed is the earliest-computed difference).
-    VDIFF_TRAIN_GRAPH_EXPERIMENTAL=1 python tools/graph_localize.py [--size 64] [--steps 4]"""
+With --lr > 0 the weights move (Adam, eager after each replay) and the parameters after each
+step are compared as well; --audio runs the wav2vec2 encoder (random init) with the host RNGs
+(torch, numpy, random) re-seeded identically before each trainer's step, so both trainers draw
+the same SpecAugment / LayerDrop decisions; --dropout sets the ResBlock dropout (the graph's
+masks come from the device counter, so with dropout the two runs differ by design).
+    python tools/graph_localize.py [--size 64] [--steps 4] [--lr 0] [--audio] [--dropout 0]"""
 import argparse
 import copy
 import json
@@ -24,7 +29,12 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--mult", default="1,2,4")
+    ap.add_argument("--lr", type=float, default=0.0)
+    ap.add_argument("--audio", action="store_true")
+    ap.add_argument("--dropout", type=float, default=0.0)
     a = ap.parse_args()
+    import random
+    import numpy as np
     os.environ["VDIFF_TRAIN_GRAPH_EXPERIMENTAL"] = "1"
     from vdiff.engine import Clip, Trainer, reinit_nonzero
     from vdiff.schedulers import LinearNoiseScheduler
@@ -35,17 +45,19 @@ def main():
     m = UNetAudio(image_size=a.size, in_channels=3, model_channels=64, out_channels=3,
                   num_res_blocks=2, attention_resolutions=(1, 2, 4)[:len(mult)],
                   channel_mult=mult, audio_feature_dim=768, projected_audio_dim=128, dims=3,
-                  use_bf16=True, audio_encoder=False, dropout=0.0)
+                  use_bf16=True, audio_encoder=a.audio, audio_encoder_pretrained=False,
+                  dropout=a.dropout)
     reinit_nonzero(m, seed=1234)
     m = m.to(dev)
     models = {"eager": m, "graph": copy.deepcopy(m)}
     sched = LinearNoiseScheduler(100, 0.00085, 0.012)
-    trs = {k: Trainer(v, sched, lr=0.0, graph=(k == "graph")) for k, v in models.items()}
+    trs = {k: Trainer(v, sched, lr=a.lr, graph=(k == "graph")) for k, v in models.items()}
     g = torch.Generator(device=dev).manual_seed(0)
     T, S = a.frames, a.size
     clip = Clip(torch.rand((1, 3, T, S, S), generator=g, device=dev) * 2 - 1,
                 torch.rand((1, 3, S, S), generator=g, device=dev) * 2 - 1,
-                torch.randn((T, 768), generator=g, device=dev),
+                ({"input_values": torch.randn((T, 4000), generator=g, device=dev)} if a.audio
+                 else torch.randn((T, 768), generator=g, device=dev)),
                 torch.randn((1, 3, T, S, S), generator=g, device=dev),
                 torch.tensor([37], device=dev))
     names = [n for n, _ in m.named_parameters()]
@@ -59,6 +71,9 @@ def main():
                 hooks = [p.register_post_accumulate_grad_hook(
                     lambda p, n=n: grads.__setitem__(n, p.grad.detach().clone()))
                     for n, p in models[k].named_parameters()]
+            torch.manual_seed(1000 + step)
+            np.random.seed(1000 + step)
+            random.seed(1000 + step)
             loss = tr.step(clip)
             for h in hooks:
                 h.remove()
@@ -75,14 +90,20 @@ def main():
                 d = (gg[n].float() - ge[n].float())
                 diff.append((n, float(d.abs().max()),
                              float(d.norm() / ge[n].float().norm().clamp_min(1e-30))))
+        wdiff = [n for (n, pe), (_, pg) in zip(models["eager"].named_parameters(),
+                                                 models["graph"].named_parameters())
+                 if not torch.equal(pe, pg)]
         line = {"step": step, "loss_eager": le, "loss_graph": lg,
+                "n_weights_differ": len(wdiff), "weights_differ": wdiff[:8],
                 "graph_active": trs["graph"].graph.g is not None,
                 "n_grads_compared": len(set(ge) & set(gg)), "n_differ": len(diff),
                 "first_differing": diff[:12]}
         print(json.dumps(line), flush=True)
         report.append(line)
-    bad = [r for r in report if r["graph_active"] and (r["n_differ"] or r["loss_eager"] != r["loss_graph"])]
-    print(json.dumps({"size": a.size, "frames": a.frames, "mult": mult, "steps_bad": len(bad)}))
+    bad = [r for r in report if r["n_differ"] or r["n_weights_differ"]
+           or r["loss_eager"] != r["loss_graph"] or not r["loss_graph"] >= 0]
+    print(json.dumps({"size": a.size, "frames": a.frames, "mult": mult, "lr": a.lr,
+                      "audio": a.audio, "dropout": a.dropout, "steps_bad": len(bad)}))
     return 1 if bad else 0
 
 
