@@ -11,7 +11,9 @@ module provides
     consumer of an LDS read;
   * `kernel_text` -- the code object wrapper (.amdhsa_kernel descriptor + metadata).
 
-Hazard distances (gfx950, measured from hipcc's own padding of the same instruction pairs):
+Hazard distances (gfx950; measured from hipcc's own padding of the same instruction pairs, the
+store-data rule from LLVM's hazard recognizer -- a VALU write of the data VGPRs of a VMEM store
+wider than 64 bits needs 2 wait states on gfx940+):
 MFMA 32x32x16 write -> VALU / VMEM / DS / MFMA-A/B read 12 wait states (16x16x32: 8); VALU write -> MFMA
 read 2; transcendental write -> VALU read 2 (one instruction between); an MFMA reading its
 own accumulator chain as srcC needs none.  Wait states are counted as issued instructions
@@ -80,7 +82,7 @@ def classify(op: str) -> str:
 
 
 class Ins:
-    __slots__ = ("text", "op", "kind", "defs", "uses", "srcc", "lds_id", "wait_lds")
+    __slots__ = ("text", "op", "kind", "defs", "uses", "srcc", "lds_id", "wait_lds", "sdata")
 
     def __init__(self, text, lds_id=None, wait_lds=()):
         self.text = text.strip()
@@ -89,6 +91,7 @@ class Ins:
         ops = self.text[len(self.op):].split(",")
         ops = [o.strip() for o in ops]
         self.srcc = set()
+        self.sdata = set()   # data VGPRs of a store wider than 64 bits
         if self.kind in ("mfma", "trans", "valu"):
             self.defs = regs_of(ops[0]) if ops and ops[0] else set()
             self.uses = set().union(*[regs_of(o) for o in ops[1:]]) if len(ops) > 1 else set()
@@ -102,6 +105,9 @@ class Ins:
         elif self.kind == "vmem":
             if "lds" in self.text.split() or self.op.startswith(("buffer_store", "global_store")):
                 self.defs, self.uses = set(), set().union(*[regs_of(o.split()[0]) for o in ops])
+                if self.op.endswith(("_dwordx3", "_dwordx4", "_b96", "_b128")) and \
+                        "lds" not in self.text.split():
+                    self.sdata = regs_of(ops[0].split()[0])
             else:
                 self.defs = regs_of(ops[0])
                 self.uses = set().union(*[regs_of(o.split()[0]) for o in ops[1:]])
@@ -124,6 +130,8 @@ class Stream:
     VALU_TO_MFMA = 2   # VALU write -> MFMA read
     TRANS_RAW = 2      # transcendental write -> VALU read
     MFMA_WAR = 12      # VALU write of an in-flight MFMA's source
+    STORE_DATA = 2     # VALU write of the data VGPRs of a VMEM store wider than 64 bits
+                       # (gfx940+: 2 wait states; LLVM GCNHazardRecognizer)
 
     def __init__(self):
         self.lines = []
@@ -165,6 +173,9 @@ class Stream:
                     need = max(need, raw - d)
                 if ins.kind in ("valu", "trans", "ds", "vmem") and ins.defs & (h.uses | h.srcc):
                     need = max(need, self.MFMA_WAR - d)
+            elif h.kind == "vmem":
+                if ins.kind in ("valu", "trans") and ins.defs & h.sdata:
+                    need = max(need, self.STORE_DATA - d)
             elif h.kind in ("valu", "trans"):
                 if ins.kind == "mfma" and (ins.uses | ins.defs) & h.defs:
                     need = max(need, self.VALU_TO_MFMA - d)
@@ -207,7 +218,7 @@ class Stream:
             self.issued_at[ins.lds_id] = self.nmfma
         if ins.kind == "mfma":
             self.nmfma += 1
-        if ins.kind in ("mfma", "valu", "trans"):
+        if ins.kind in ("mfma", "valu", "trans") or ins.sdata:
             self.hist.append((self.pos, ins))
             if len(self.hist) > 64:
                 self.hist = self.hist[-64:]
