@@ -1870,10 +1870,12 @@ int cfg_from_env() {
 }
 std::atomic<int> g_cfg{cfg_from_env()};  // -1: per-kernel default (vd_attention_set_config)
 
-// D = 256 hand-scheduled dQ as the default: off until measured on the GPU (VDIFF_ASM256=1)
+// D = 256 hand-scheduled backward as the default (round 4; VDIFF_ASM256=0 restores the
+// compiled base dQ / role-split dK/dV): dQ 0.506 -> 0.339 ms, dK/dV 0.804 -> 0.458 ms at
+// N = 16384 on one box (tools/gpu_r04f.sh, profiles/r04f_ab_asm256_timing.txt)
 const bool g_asm256 = [] {
   const char* e = getenv("VDIFF_ASM256");
-  return e && atoi(e) == 1;
+  return !(e && atoi(e) == 0);
 }();
 
 AttnCfg pick_cfg(int D, bool bf16, int kind) {
@@ -1891,6 +1893,8 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //   D = 128 backward (round 3): hand-scheduled dQ 2.55-2.60 / dK/dV 3.37-3.40 ms vs W8 2.96 /
   //            PAIR 3.97-3.99 ms on the same box (tools/gpu_asm128.sh); forward 1.67-1.68 vs
   //            D8N 2.04-2.05 ms (tools/gpu_r03c.sh)
+  //   D = 256 backward (round 4): hand-scheduled dQ 0.339 / dK/dV 0.458 ms vs base 0.506 /
+  //            ROLE 0.804 ms (tools/gpu_r04f.sh)
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only

@@ -878,11 +878,118 @@ __device__ __forceinline__ int wg_off(int r, int c) {  // element offset of chan
   return r * 64 + ((((c >> 3) ^ wg_swz(r)) << 3) | (c & 7));
 }
 
+// The KS form of wgrad_dma_kernel's main loop and epilogue (see there).  Wave w = wk * WCO +
+// wco takes co [64 wco, +64) of the tile and the k-steps kb = wk * (4 / KSN) + kk of every
+// 64-pixel step.  Fragments as in the 16x16x32 form: within each 16-lane group a lane passes
+// (row base + q4, column base + 4 p4) to ds_read_b64_tr_b16 and gets column base + fr of the
+// four rows; 32x32x16 operands: co / ci = 16 (G & 1) + fr, pixels 8 (G >> 1) + 0..7, G = lane / 16.
+template <int RW, int COT, int NST, int PIECES, int STAGE, int Y_BYTES, typename Issue>
+__device__ __forceinline__ void wgrad_ks_body(const WgtGeom& g, int wc, int SW, char* smem,
+                                              const bf16_t* lds, int wave, int lane,
+                                              int nsteps, Issue& issue, float* __restrict__ dw,
+                                              int wsplit, int co0, int ci0, int tab) {
+  constexpr int WCO = COT / 64, KSN = 4 / WCO, KPW = 4 / KSN;
+  const int wco = wave % WCO, wk = wave / WCO;
+  f32x16 acc[3][2][2];
+#pragma unroll
+  for (int tc = 0; tc < 3; ++tc)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[tc][i][j][r] = 0.f;
+  vm_drain();
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s);
+  const int G = lane >> 4, fr = lane & 15, q4 = fr >> 2, p4 = fr & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    vm_wait_barrier<(NST - 2) * PIECES>();
+    issue(s + NST - 1);
+    const bf16_t* Ys = lds + (s % NST) * (STAGE / 2);
+    const bf16_t* Xs = Ys + Y_BYTES / 2;
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int kb = wk * KPW + kk;
+      const int p_lo = 16 * kb + 8 * (G >> 1) + q4, p_hi = p_lo + 4;
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = wco * 64 + 32 * i + 16 * (G & 1) + 4 * p4;
+        const bf16_t* plane = Ys + (c >> 6) * 4096;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_bf16x4*)(plane + wg_off(p_lo, c & 63)));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_bf16x4*)(plane + wg_off(p_hi, c & 63)));
+        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int s_lo = (p_lo / wc) * SW + p_lo % wc, s_hi = (p_hi / wc) * SW + p_hi % wc;
+#pragma unroll
+      for (int tc = 0; tc < 3; ++tc) {
+        bf16x8 bfr[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = 32 * j + 16 * (G & 1) + 4 * p4;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(Xs + wg_off(s_lo + tc, c)));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(Xs + wg_off(s_hi + tc, c)));
+          bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[tc][i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[tc][i][j], 0, 0, 0);
+      }
+    }
+  }
+  vm_drain();
+  __syncthreads();  // every wave is done with the ring: its LDS holds the reduction
+  // per tap: the four waves' 64 x 64 partial tiles [wave][blk = 2 i + j][r][lane] (64 KiB),
+  // then the KSN waves of each co half add theirs in wave order, pair (blk, r) by pair
+  float* red = reinterpret_cast<float*>(smem);
+  const int taps = g.kt * g.kh * g.kw;
+  const int64_t krow = (int64_t)taps * g.Ci;
+#pragma unroll
+  for (int tc = 0; tc < 3; ++tc) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          red[((wave * 4 + 2 * i + j) * 16 + r) * 64 + lane] = acc[tc][i][j][r];
+    __syncthreads();
+    const int tap = tab * g.kw + tc;
+    for (int idx = wk; idx < 64; idx += KSN) {
+      const int blk = idx >> 4, r = idx & 15;
+      float v = red[((wco * 4 + blk) * 16 + r) * 64 + lane];
+#pragma unroll
+      for (int k = 1; k < KSN; ++k) v += red[(((wco + WCO * k) * 4 + blk) * 16 + r) * 64 + lane];
+      const int co = co0 + wco * 64 + 32 * (blk >> 1) + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+      const int ci = ci0 + 32 * (blk & 1) + (lane & 31);
+      if (co < g.Co && ci < g.Ci)
+        wg_out(g, dw, wsplit, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, v);
+    }
+    __syncthreads();
+  }
+}
+
 // PLANE (round 2): all nine (kh, kw) taps of one kt per workgroup -- the X strip holds the
 // three input rows above / at / below the step's 64-pixel output row (W % 64 == 0, so a step
 // is one row segment), and one dY tile feeds nine taps instead of three.
-template <int RW, int COT, int NST, bool ONE, bool PLANE = false>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
-__global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
+//
+// KS (round 4): the four waves split each 64-pixel step's reduction (16 pixels = one k-step
+// of v_mfma_f32_32x32x16_bf16 each, COT = 64; COT = 128: two co halves x two k-halves)
+// instead of the output tile, so every wave owns a 64 co x 64 ci x 3-tap tile (192 fp32
+// accumulators, one wave per SIMD).  Per 384 MFMA cycles a wave then reads 8 KiB of
+// transposed fragments instead of 16 KiB: the COT = 64 form needs 128 B/clk of LDS per CU at
+// the MFMA rate (two workgroups per CU), the LDS peak, and is LDS-bound; this one needs 64.
+// The waves' partial tiles are added through LDS after the loop, in wave order (fixed).
+template <int RW, int COT, int NST, bool ONE, bool PLANE = false, bool KS = false>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
+__global__ __launch_bounds__(kThreads, (PLANE || KS) ? 1 : 2) void wgrad_dma_kernel(
     WgtGeom g, int wc, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
     float* __restrict__ dw) {
   constexpr int PY = COT / 32, PX = RW / 32;  // pieces per wave per step
@@ -1008,6 +1115,12 @@ __global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
     }
   };
 
+  if constexpr (KS) {
+    static_assert(!ONE && !PLANE && (COT == 64 || COT == 128), "KS: kw-strip tiles");
+    wgrad_ks_body<RW, COT, NST, PIECES, STAGE, Y_BYTES>(g, wc, SW, smem, lds, wave, lane, nsteps,
+                                                        issue, dw, wsplit, co0, ci0, tab);
+    return;
+  }
   // wave tile: co [WTM wm, +WTM) x ci [32 wn, +32) x 3 taps
   const int wm = wave & 1, wn = wave >> 1;
   f32x4 acc[NT][NI][2];
@@ -1993,6 +2106,11 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
       return e ? atoi(e) : 0;
     }();
     const bool plane = !one && wplane && d->Wo % 64 == 0;
+    // K-split waves for the kw-strip tiles (wgrad_ks_body; A/B knob VDIFF_WGRAD_KS)
+    static const int wks = [] {
+      const char* e = getenv("VDIFF_WGRAD_KS");
+      return e ? atoi(e) : 0;
+    }();
     const int64_t tiles = (int64_t)vd_cdiv(d->Co, cot) * vd_cdiv(d->Ci, 64) *
                           (one ? 1 : (plane ? d->kt : d->kt * d->kh));
     // ~2048 workgroups, but at least 32 K steps each for the strip kernel (shorter pixel
@@ -2021,14 +2139,22 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
 #define VD_WGD(RW, COT, NST, ONE, ...)                                                     \
   do {                                                                                     \
     auto kern = wgrad_dma_kernel<RW, COT, NST, ONE, ##__VA_ARGS__>;                        \
-    const int lds = NST * (COT + RW) * 128;                                                \
+    const int lds = std::max(NST * (COT + RW) * 128, wks ? 65536 : 0);                     \
     (void)hipFuncSetAttribute((const void*)kern,                                           \
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
     kern<<<grid, kThreads, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);     \
   } while (0)
     // 64 x 64 tiles, double-buffered (40 KiB at RW = 96: three workgroups per CU).
     // Measured against COT = 128 and a three-stage ring: both slower (tools/conv_ab.sh).
-    if (one && cot == 192 && w1_nst >= 4) VD_WGD(64, 192, 4, true);
+    if (wks && !one && !plane) {  // K-split waves (A/B: VDIFF_WGRAD_KS=1)
+      if (cot == 128 && rows <= 96) VD_WGD(96, 128, 3, false, false, true);
+      else if (cot == 128 && rows <= 128) VD_WGD(128, 128, 3, false, false, true);
+      else if (cot == 128) VD_WGD(192, 128, 3, false, false, true);
+      else if (rows <= 96) VD_WGD(96, 64, 4, false, false, true);
+      else if (rows <= 128) VD_WGD(128, 64, 4, false, false, true);
+      else VD_WGD(192, 64, 3, false, false, true);
+    }
+    else if (one && cot == 192 && w1_nst >= 4) VD_WGD(64, 192, 4, true);
     else if (one && cot == 192) VD_WGD(64, 192, 2, true);
     else if (one && cot == 128 && w1_nst >= 4) VD_WGD(64, 128, 4, true);
     else if (one && cot == 128) VD_WGD(64, 128, 2, true);

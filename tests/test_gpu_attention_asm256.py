@@ -1,6 +1,6 @@
 """The hand-scheduled head_dim-256 backward kernels (csrc/asm/gen_d256.py vd_attn_bwd_dq_d256,
-gen_d256dk.py vd_attn_bwd_dkdv_d256; attention config "asm" at D = 256, the default with
-VDIFF_ASM256=1) against the compiler-scheduled kernels that run the same products in the same
+gen_d256dk.py vd_attn_bwd_dkdv_d256; attention config "asm" at D = 256, the default since
+round 4 unless VDIFF_ASM256=0) against the compiler-scheduled kernels that run the same products in the same
 order -- dQ: the 4-wave kernel (config "base": the same 32-key blocks, key split into fp32
 partials and partial sum); dK / dV: the role-split wave pairs (config "role") -- and a
 materialised fp32 reference of QKVAttentionLegacy's backward (unet.py:349-366 at C = 256, the
@@ -8,6 +8,7 @@ materialised fp32 reference of QKVAttentionLegacy's backward (unet.py:349-366 at
 Shapes: whole and ragged tiles, a batch of two sequences, the spatial grouping (groups on
 grid.y), the config-2 length 16384 and 16384 + 17; the kernels take N >= 1024."""
 import math
+import os
 
 import pytest
 import torch
@@ -51,7 +52,10 @@ def test_asm256_dq_equals_compiled_kernel(B, N, seed):
     assert b.abs().max() > 0
     err = float((a - b).norm() / a.norm())
     print(f"asm256 dQ vs base B={B} N={N}: rel-L2 {err:.2e}")
-    assert err <= 1e-5, err
+    # bit-exact where both kernels take the same key-split count (batch r04e: 0.0 at N = 1024
+    # .. 16384); where the counts differ the fp32 partials are summed in another grouping
+    # (2e-5 at N = 16401)
+    assert err <= 1e-4, err
     # dK / dV: the column-split kernel ("base") and the asm role split agree to rounding
     assert _rel(g1[:, C:], g0[:, C:]) <= 4e-3
 
@@ -68,7 +72,8 @@ def test_asm256_dkdv_equals_role_kernel(B, N, seed):
         assert b.abs().max() > 0, name
         err = float((a - b).norm() / a.norm())
         print(f"asm256 {name} vs role B={B} N={N}: rel-L2 {err:.2e}")
-        assert err <= 1e-5, (name, err)
+        # bit-exact where both take the same query-split count, 2e-5..4e-5 where they do not
+        assert err <= 1e-4, (name, err)
 
 
 def test_asm256_spatial_groups():
@@ -76,9 +81,9 @@ def test_asm256_spatial_groups():
     kw = dict(mode="spatial", spatial=(4, 32, 32))
     g0 = _grads(qkv, g, "base", **kw)
     g1 = _grads(qkv, g, "asm", **kw)
-    assert _rel(g1[:, :C], g0[:, :C]) <= 1e-5
+    assert _rel(g1[:, :C], g0[:, :C]) <= 1e-4
     g0 = _grads(qkv, g, "role", **kw)
-    assert _rel(g1[:, C:], g0[:, C:]) <= 1e-5
+    assert _rel(g1[:, C:], g0[:, C:]) <= 1e-4
 
 
 def test_asm256_against_fp32_reference():
@@ -95,6 +100,7 @@ def test_asm256_against_fp32_reference():
         assert e < 2e-2, e
 
 
+@pytest.mark.skipif(os.environ.get("VDIFF_ASM256") == "0", reason="compiled kernels selected")
 def test_asm256_is_the_d256_default():
     qkv, g = _inputs(1, 2048, 9)
     assert torch.equal(_grads(qkv, g, "auto"), _grads(qkv, g, "asm"))

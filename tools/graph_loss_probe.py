@@ -9,7 +9,9 @@ dropout 0, lr 1e-2); per step after the replay this reads, with a sync between e
   returned   the value Trainer.step returned
 and checks the packed-operand plan: every descriptor's source and destination pointer must be
 a live parameter / plan buffer, and the loss buffer must lie outside every plan buffer.
-    python tools/graph_loss_probe.py [--steps 7] [--twin]"""
+--keep-pred 0 / --sync 0 drop the prediction reference / the synchronised reads (both 0: the
+product's own TrainStepGraph.step).
+    python tools/graph_loss_probe.py [--steps 7] [--twin] [--keep-pred 0|1] [--sync 0|1]"""
 import argparse
 import json
 import os
@@ -28,6 +30,8 @@ def main():
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--steps", type=int, default=7)
     ap.add_argument("--twin", action="store_true", help="an eager twin trainer alternates")
+    ap.add_argument("--keep-pred", type=int, default=1, help="keep the prediction buffer alive")
+    ap.add_argument("--sync", type=int, default=1, help="synchronise and read after the replay")
     a = ap.parse_args()
     os.environ["VDIFF_TRAIN_GRAPH_EXPERIMENTAL"] = "1"
     import copy
@@ -63,7 +67,8 @@ def main():
         with tr_.packs:
             xt = tr_.scheduler.add_noise(self.x0, self.eps, self.t)
             pred = tr_.model(xt, self.cond, self.feats, self.t)
-            self.pred = pred.detach()  # keeps the graph's prediction buffer alive
+            if a.keep_pred:
+                self.pred = pred.detach()  # keeps the graph's prediction buffer alive
             loss = F.mse_loss(pred, self.eps)
             loss.backward()
         return loss.detach()
@@ -79,13 +84,15 @@ def main():
                              (self.cond, clip_.cond), (self.feats, enc)):
                 dst.copy_(src)
         self.g.replay()
-        torch.cuda.synchronize()
-        probe["loss_out"] = float(self.loss)
-        probe["mse_pred"] = float(F.mse_loss(self.pred, self.eps))
-        probe["pred_dtype"] = str(self.pred.dtype)
+        if a.sync:
+            torch.cuda.synchronize()
+            probe["loss_out"] = float(self.loss)
+            if a.keep_pred:
+                probe["mse_pred"] = float(F.mse_loss(self.pred, self.eps))
         self.tr.opt.step()
-        torch.cuda.synchronize()
-        probe["loss_after"] = float(self.loss)
+        if a.sync:
+            torch.cuda.synchronize()
+            probe["loss_after"] = float(self.loss)
         self.steps += 1
         loss = self.loss.clone()
         self.tr._track_finite(loss)
@@ -99,7 +106,7 @@ def main():
             le = float(tw.step(clip))
         else:
             le = None
-        if tr.graph.g is not None:
+        if tr.graph.g is not None and (a.sync or a.keep_pred):
             G.step = probe_step
         lr_ = tr.step(clip)
         G.step = orig_step

@@ -2,9 +2,9 @@
 3x3x3 stride-1 and 1x1 shape of the step with its per-step launch count, through
 vd_conv3d_bwd_weight_det (fixed-order split-K, the default) or vd_conv3d_bwd_weight (atomics,
 VDIFF_WGRAD_ATOMIC=1), timed with HIP events; the grid layout follows VDIFF_WGRAD_XCD (read
-once per process).  Checked against torch's fp32 weight gradient (3x3x3 on a frame slab, 1x1
-whole).  Prints per-shape microseconds / TFLOP/s and the per-step totals.
-    VDIFF_WGRAD_XCD=0|1 [VDIFF_WGRAD_ATOMIC=1] python tools/wgrad_ab.py"""
+once per process).  Checked against the fp32 parity-mode weight gradient of the same values on
+the device (whole tensors).  Prints per-shape microseconds / TFLOP/s and the per-step totals.  VDIFF_WGRAD_KS=1 selects the K-split-wave kw-strip kernel (wgrad_ks_body).
+    VDIFF_WGRAD_XCD=0|1 [VDIFF_WGRAD_ATOMIC=1] [VDIFF_WGRAD_KS=1] python tools/wgrad_ab.py"""
 import os
 import sys
 
@@ -28,7 +28,8 @@ SHAPES = ((256, 256, 3, 32, 16, 10), (64, 64, 3, 128, 16, 7), (128, 128, 3, 64, 
 
 def main():
     atomic = os.environ.get("VDIFF_WGRAD_ATOMIC", "0") == "1"
-    tag = f"xcd={os.environ.get('VDIFF_WGRAD_XCD', '1')} {'atomic' if atomic else 'det'}"
+    tag = (f"xcd={os.environ.get('VDIFF_WGRAD_XCD', '1')} {'atomic' if atomic else 'det'}"
+           f"{' ks' if os.environ.get('VDIFF_WGRAD_KS', '0') == '1' else ''}")
     tot3 = tot1 = 0.0
     worst = 0.0
     for Ci, Co, k, H, T, per in SHAPES:
@@ -56,18 +57,17 @@ def main():
                 _lib.call("vd_conv3d_bwd_weight_det", d, x.data_ptr(), dy.data_ptr(),
                           dw.data_ptr(), Co, Ci, ws.data_ptr(), ws.numel(), st)
         run()
-        # reference on a slab of frames (3x3x3 taps see t-1..t+1 only)
-        ts = min(T, 4)
-        xr = x[:, :ts].float().permute(0, 4, 1, 2, 3).cpu()
-        dyr = dy[:, :ts].float().permute(0, 4, 1, 2, 3).cpu()
-        if ts == T:
-            ref = torch.nn.grad.conv3d_weight(xr, (Co, Ci, k, k, k), dyr, padding=p)
-            got = dw.cpu() if not atomic else dw.cpu().permute(0, 2, 1)
-            got = got.reshape(ref.shape)
-            err = float((got - ref).norm() / ref.norm())
-            worst = max(worst, err)
-        else:
-            err = float("nan")
+        # reference: the fp32 parity-mode weight gradient (conv_wgrad_kernel, exact-fp32 MFMA;
+        # torch-checked in tests/test_gpu_conv.py) on the same bf16 values, whole tensors
+        xr, dyr = x.float().contiguous(), dy.float().contiguous()
+        d32 = ops._desc(1, [T, H, H], Ci, [T, H, H], Co, [k] * 3 if k == 3 else [1, 1, 1],
+                        [1, 1, 1], [p] * 3, ops._DT[torch.float32])
+        ref = torch.zeros(Co, taps, Ci, dtype=torch.float32, device="cuda")
+        _lib.call("vd_conv3d_bwd_weight", d32, xr.data_ptr(), dyr.data_ptr(), ref.data_ptr(), st)
+        got = dw.permute(0, 2, 1) if not atomic else dw
+        err = float((got - ref).norm() / ref.norm())
+        worst = max(worst, err)
+        del xr, dyr, ref
         for _ in range(3):
             run()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
