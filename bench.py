@@ -77,12 +77,15 @@ def parse():
     ap.add_argument("--vivit-batch", type=int, default=16, help="clips per GPU (reference: 16)")
     ap.add_argument("--vivit-eager", action="store_true",
                     help="no HIP-graph capture of the ViViT step")
-    ap.add_argument("--vivit-eager-ddp", action="store_true",
-                    help="N > 1: eager ViViT step with the bucketed all-reduce instead of the "
-                         "graph replays around one all-reduce")
-    ap.add_argument("--xattn-steps", type=int, default=3,
+    ap.add_argument("--vivit-graph-ddp", action="store_true",
+                    help="N > 1: graph replays around one all-reduce instead of the eager step "
+                         "with the bucketed all-reduce (rehearsed over gloo only, so opt-in)")
+    ap.add_argument("--xattn-steps", type=int, default=-1,
                     help="timed train steps with audio cross-attention (build extension, "
-                         "auxiliary leg); 0 skips it")
+                         "auxiliary leg) after --warmup untimed ones, from the benchmark init "
+                         "at --lr like the headline; -1 (default): --steps, so both legs time "
+                         "the same step indices (the clock follows the weights, DESIGN 5); "
+                         "0 skips it")
     ap.add_argument("--train-graph", action="store_true",
                     help="auxiliary leg: graph-replayed train step paired with an eager one "
                          "(DESIGN section 9 item 3)")
@@ -326,10 +329,10 @@ def vivit_leg(args, rank, world, device):
     torch.manual_seed(4321)
     model = ViViT(VivitModel(cfg, use_bf16=args.dtype == "bf16"), 40, 5).to(device)
     broadcast_parameters(model)
-    # one process: the whole step as one HIP graph.  N > 1: forward + backward graph, ONE
-    # all-reduce of the flattened gradients, AdamW graph (VivitTrainer); --vivit-eager-ddp
-    # runs eager with the bucketed all-reduce instead
-    graph = not args.vivit_eager and (world == 1 or not args.vivit_eager_ddp)
+    # one process: the whole step as one HIP graph.  N > 1: eager with the bucketed
+    # all-reduce; --vivit-graph-ddp: forward + backward graph, ONE all-reduce of the flattened
+    # gradients, AdamW graph (VivitTrainer) -- not yet run over RCCL (advisor r03)
+    graph = not args.vivit_eager and (world == 1 or args.vivit_graph_ddp)
     tr = VivitTrainer(model, graph=graph)
     g = torch.Generator(device=device).manual_seed(300 + rank)
     B = args.vivit_batch
@@ -377,19 +380,24 @@ def xattn_leg(args, rank, world, device, base_ms):
     model = build_model(args, device, audio_attention=True)
     broadcast_parameters(model)
     work = unet_forward_work(model, (args.clips_per_gpu, 195, args.frames, args.size, args.size))
-    tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2)
+    tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=args.lr)
     clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
-    for _ in range(2):
-        tr.step(clip)
+    nsteps = args.steps if args.xattn_steps < 0 else args.xattn_steps
+    losses = []
+    for _ in range(args.warmup):
+        losses.append(tr.step(clip))
     barrier_sync(world)
     t0 = time.perf_counter()
-    for _ in range(args.xattn_steps):
-        loss = tr.step(clip)
+    for _ in range(nsteps):
+        losses.append(tr.step(clip))
     barrier_sync(world)
     el = max_over_ranks(time.perf_counter() - t0, world, device)
-    ms = el / args.xattn_steps * 1e3
+    ms = el / nsteps * 1e3
+    loss = losses[-1]
     out = {"metric": "train-step frames/sec with audio cross-attention (build extension)",
-           "value": round(world * args.clips_per_gpu * args.frames * args.xattn_steps / el, 4),
+           "value": round(world * args.clips_per_gpu * args.frames * nsteps / el, 4),
+           "steps": nsteps, "warmup": args.warmup,
+           "train_losses": [_num(x, 5) for x in losses],
            "unit": "frames/s", "ms_per_step": round(ms, 2),
            "overhead_ms_vs_concat_only": round(ms - base_ms, 2) if base_ms else None,
            "fwd_tflop_per_clip": round(work.total / 1e12, 3), "audio_tokens_per_frame": 12,
@@ -659,7 +667,7 @@ def main():
         if "value" not in result:
             result.update(value=ddim["value"], unit="steps/s", ms_per_step=ddim["ms_per_step"])
 
-    if args.only in ("train", "all") and args.xattn_steps > 0:
+    if args.only in ("train", "all") and args.xattn_steps != 0:
         try:  # an auxiliary leg: never let it take the headline numbers down
             result["audio_xattn"] = xattn_leg(args, rank, world, device,
                                               result.get("ms_per_step"))

@@ -176,7 +176,8 @@ class TrainStepGraph:
 
     Captured: the batched weight pack, q_sample, the conditioning concat and the UNet forward,
     the MSE and the whole backward down to the UNet parameters' gradients and the gradient of
-    the pooled audio features.  Eager around it: the wav2vec2 encoder (transformers draws its
+    the pooled audio features; the reported loss is the eager MSE of the replayed prediction
+    (_body).  Eager around it: the wav2vec2 encoder (transformers draws its
     LayerDrop and SpecAugment decisions on the host every step, which changes the launch
     sequence, so it cannot be frozen), its backward (fed the replayed feature gradient) and
     the fused Adam step over all parameters.  Same math as the eager step: the first `warmup`
@@ -221,7 +222,10 @@ class TrainStepGraph:
         for p in self.eager_params:
             p.grad = None
         self.steps += 1
-        loss = self.loss.clone()
+        # the loss is computed here, eagerly, from the replay's own prediction: the MSE the
+        # graph captured is only the backward's seed (see _body)
+        with torch.no_grad():
+            loss = F.mse_loss(self.pred, self.eps)
         tr._track_finite(loss)
         return loss
 
@@ -230,13 +234,21 @@ class TrainStepGraph:
         return tuple((tuple(x.shape), x.dtype) for x in (clip.x0, clip.eps, clip.t, clip.cond, enc))
 
     def _body(self):
+        """The captured region.  Its MSE seeds the backward only (d mean((p - e)^2) / dp does
+        not read the forward's value): the forward VALUE of torch's multi-block mean, replayed
+        in this graph, came out wrong from the third replay on in runs whose host code did
+        other GPU reductions between replays (round 4: -0.855 for 9.03 at 64x64x16, while every
+        gradient and every weight stayed bit-identical to the eager step; the value was already
+        wrong when copied out right after the MSE, inside the graph; tools/graph_loss_probe.py,
+        profiles/r04j_graph_loss_probe.txt).  step() therefore reports the MSE of the kept
+        prediction buffer, computed eagerly -- the eager step's own op on the same values."""
         tr = self.tr
         with tr.packs:
             xt = tr.scheduler.add_noise(self.x0, self.eps, self.t)
             pred = tr.model(xt, self.cond, self.feats, self.t)
+            self.pred = pred.detach()  # lives in the graph's pool, rewritten by each replay
             loss = F.mse_loss(pred, self.eps)
             loss.backward()
-        return loss.detach()
 
     def _capture(self, clip, enc):
         from . import _lib
@@ -260,13 +272,11 @@ class TrainStepGraph:
         self.feats.grad = None
         self.g = torch.cuda.CUDAGraph()
         lib = _lib.lib()
-        # the graph's loss output goes to a buffer allocated outside its memory pool
-        self.loss = torch.zeros((), dtype=torch.float32, device=enc.device)
         lib.vd_set_dropout_counter(self.ctr.data_ptr())
         try:
             with torch.cuda.graph(self.g, capture_error_mode="thread_local"):
                 self.ctr.add_(1)
-                self.loss.copy_(self._body())
+                self._body()
         finally:
             lib.vd_set_dropout_counter(None)
         self.shapes = self._shapes(clip, enc)

@@ -210,3 +210,103 @@ def test_dropout_counter_mixes_into_seed():
     y0, _ = run(123)
     assert torch.equal(y1, y2) and torch.equal(d1, d2)
     assert not torch.equal(y1, y0)
+
+
+# ------------------------------------------------------------------ config-2 scale (round 4)
+def _bench_unet(size, dropout):
+    """The bench model (config 2 topology, bf16, joint attention) without the wav2vec2
+    encoder: pooled audio features in, so both trainers see identical inputs."""
+    from vdiff.engine import reinit_nonzero
+    from vdiff.unet_audio import UNetAudio
+    torch.manual_seed(1234)
+    m = UNetAudio(image_size=size, in_channels=3, model_channels=64, out_channels=3,
+                  num_res_blocks=2, attention_resolutions=(1, 2, 4), channel_mult=(1, 2, 4),
+                  audio_feature_dim=768, projected_audio_dim=128, dims=3, use_bf16=True,
+                  audio_encoder=False, dropout=dropout)
+    reinit_nonzero(m, seed=1234)
+    return m.to(dev)
+
+
+def _bench_clip(size, frames=16):
+    from vdiff.engine import Clip
+    g = torch.Generator(device=dev).manual_seed(0)
+    return Clip(torch.rand((1, 3, frames, size, size), generator=g, device=dev) * 2 - 1,
+                torch.rand((1, 3, size, size), generator=g, device=dev) * 2 - 1,
+                torch.randn((frames, 768), generator=g, device=dev),
+                torch.randn((1, 3, frames, size, size), generator=g, device=dev),
+                torch.tensor([37], device=dev))
+
+
+def test_graph_config2_lr0_replays_equal_eager():
+    """VERDICT r03 item 3 at the config-2 shape (128x128x16, bf16, joint attention): two
+    eager warm-up steps, the capture, three replays.  With every reduction fixed-order the
+    replayed step equals the eager step bit for bit -- the loss and every gradient -- and the
+    loss is a finite, non-negative mean of squares."""
+    from vdiff.engine import Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    m = _bench_unet(128, 0.0)
+    models = {"eager": m, "graph": copy.deepcopy(m)}
+    sched = LinearNoiseScheduler(100, 0.00085, 0.012)
+    trs = {k: Trainer(v, sched, lr=0.0, graph=(k == "graph")) for k, v in models.items()}
+    clip = _bench_clip(128)
+    for step in range(5):
+        ge = {}
+        hooks = [p.register_post_accumulate_grad_hook(
+            lambda p, n=n: ge.__setitem__(n, p.grad.detach().clone()))
+            for n, p in models["eager"].named_parameters()]
+        le = trs["eager"].step(clip)
+        for h in hooks:
+            h.remove()
+        lg = trs["graph"].step(clip)
+        torch.cuda.synchronize()
+        assert torch.isfinite(lg) and float(lg) >= 0.0, (step, float(lg))
+        assert torch.equal(le, lg), (step, float(le), float(lg))
+        if trs["graph"].graph.g is not None:
+            for n, p in models["graph"].named_parameters():
+                assert torch.equal(p.grad, ge[n]), (step, n)
+    assert trs["graph"].graph.steps == 5 and trs["graph"].graph.g is not None
+
+
+def test_graph_loss_with_moving_weights_and_host_reductions():
+    """The round-4 reproducer of the negative replay losses: 64x64x16, lr 1e-2 (the weights
+    move), an eager twin stepped alternately, and torch.equal over every parameter pair after
+    each step (host-side GPU reductions between the replays).  Before the fix the replayed
+    step returned -0.855 and -0.707 (bf16-exact garbage) at steps 4-5 while every weight and
+    gradient stayed bit-identical; the loss now comes from the replay's prediction and must
+    equal the twin's exactly at every step."""
+    from vdiff.engine import Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    m = _bench_unet(64, 0.0)
+    twin = copy.deepcopy(m)
+    sched = LinearNoiseScheduler(100, 0.00085, 0.012)
+    tg = Trainer(m, sched, lr=1e-2, graph=True)
+    te = Trainer(twin, sched, lr=1e-2)
+    clip = _bench_clip(64)
+    for step in range(8):
+        le = float(te.step(clip))
+        lg = float(tg.step(clip))
+        assert lg >= 0.0 and lg == le, (step, le, lg)
+        assert all(torch.equal(a, b) for a, b in zip(twin.parameters(), m.parameters())), step
+
+
+def test_graph_config2_dropout_replays():
+    """Config-2 shape with the ResBlock dropout at 0.1 and lr 0: three replays draw fresh
+    masks through the device step counter (so they are not comparable to the eager steps,
+    whose masks come from host seeds); each replayed loss is finite, non-negative, differs
+    from the previous replay's, and stays within the spread of eager dropout steps."""
+    from vdiff.engine import Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    m = _bench_unet(128, 0.1)
+    twin = copy.deepcopy(m)
+    sched = LinearNoiseScheduler(100, 0.00085, 0.012)
+    tg = Trainer(m, sched, lr=0.0, graph=True)
+    te = Trainer(twin, sched, lr=0.0)
+    clip = _bench_clip(128)
+    eager = [float(te.step(clip)) for _ in range(5)]
+    graph = [float(tg.step(clip)) for _ in range(5)]
+    assert tg.graph.g is not None
+    lo, hi = min(eager), max(eager)
+    for i, v in enumerate(graph):
+        assert v == v and v >= 0.0, (i, v)
+        assert 0.5 * lo <= v <= 2.0 * hi, (i, v, eager)
+    assert len(set(graph[2:])) == 3, graph

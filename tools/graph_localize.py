@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--audio", action="store_true")
     ap.add_argument("--dropout", type=float, default=0.0)
+    ap.add_argument("--no-grads", action="store_true",
+                    help="compare losses and weights only (no gradient copies)")
+    ap.add_argument("--loss-first", action="store_true",
+                    help="read the returned loss right after the step, before the copies")
     a = ap.parse_args()
     import random
     import numpy as np
@@ -67,7 +71,7 @@ def main():
         for k, tr in trs.items():
             grads = {}
             hooks = []
-            if k == "eager":  # graph grads are read from p.grad after the replay
+            if k == "eager" and not a.no_grads:  # graph grads: p.grad after the replay
                 hooks = [p.register_post_accumulate_grad_hook(
                     lambda p, n=n: grads.__setitem__(n, p.grad.detach().clone()))
                     for n, p in models[k].named_parameters()]
@@ -75,13 +79,17 @@ def main():
             np.random.seed(1000 + step)
             random.seed(1000 + step)
             loss = tr.step(clip)
+            lval = float(loss) if a.loss_first else None
             for h in hooks:
                 h.remove()
-            if k == "graph" and tr.graph.g is not None:
+            if k == "graph" and tr.graph.g is not None and not a.no_grads:
                 grads = {n: p.grad.detach().clone() for n, p in models[k].named_parameters()
                          if p.grad is not None}
             torch.cuda.synchronize()
-            rec[k] = (float(loss), grads)
+            rec[k] = (float(loss) if lval is None else lval, grads)
+            if lval is not None and lval != float(loss):
+                print(json.dumps({"step": step, "trainer": k, "loss_changed_after_copies":
+                                  [lval, float(loss)]}), flush=True)
         le, ge = rec["eager"]
         lg, gg = rec["graph"]
         diff = []

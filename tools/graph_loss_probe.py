@@ -9,8 +9,8 @@ dropout 0, lr 1e-2); per step after the replay this reads, with a sync between e
   returned   the value Trainer.step returned
 and checks the packed-operand plan: every descriptor's source and destination pointer must be
 a live parameter / plan buffer, and the loss buffer must lie outside every plan buffer.
---keep-pred 0 / --sync 0 drop the prediction reference / the synchronised reads (both 0: the
-product's own TrainStepGraph.step).
+--sync 0 drops the synchronised reads; --keep-pred 0 --sync 0 runs the product's own
+TrainStepGraph.step (since round 4 it reports the eager MSE of the kept prediction).
     python tools/graph_loss_probe.py [--steps 7] [--twin] [--keep-pred 0|1] [--sync 0|1]"""
 import argparse
 import json
@@ -30,8 +30,18 @@ def main():
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--steps", type=int, default=7)
     ap.add_argument("--twin", action="store_true", help="an eager twin trainer alternates")
-    ap.add_argument("--keep-pred", type=int, default=1, help="keep the prediction buffer alive")
+    ap.add_argument("--keep-pred", type=int, default=1,
+                    help="1: report the old in-graph loss output from the probe's own step; "
+                         "0 (with --sync 0 and no --snap): the product's step, which reports the "
+                         "eager MSE of the replayed prediction (round-4 fix)")
     ap.add_argument("--sync", type=int, default=1, help="synchronise and read after the replay")
+    ap.add_argument("--seed-each-step", action="store_true",
+                    help="torch / numpy / random re-seeded before every step (graph_localize)")
+    ap.add_argument("--snap", action="store_true",
+                    help="inside the graph: copy the MSE to a second buffer before the "
+                         "backward; after the replay: clone the loss output before Adam")
+    ap.add_argument("--compare-weights", action="store_true",
+                    help="torch.equal of every parameter pair after each step (needs --twin)")
     a = ap.parse_args()
     os.environ["VDIFF_TRAIN_GRAPH_EXPERIMENTAL"] = "1"
     import copy
@@ -63,15 +73,18 @@ def main():
     orig_body, orig_step = G._body, G.step
 
     def body(self):
+        # the round-4 product body plus the old design's in-graph loss output (self.loss, a
+        # buffer outside the graph pool, written by a copy after the backward)
         tr_ = self.tr
         with tr_.packs:
             xt = tr_.scheduler.add_noise(self.x0, self.eps, self.t)
             pred = tr_.model(xt, self.cond, self.feats, self.t)
-            if a.keep_pred:
-                self.pred = pred.detach()  # keeps the graph's prediction buffer alive
+            self.pred = pred.detach()
             loss = F.mse_loss(pred, self.eps)
+            if a.snap:
+                self.loss_pre.copy_(loss.detach())
             loss.backward()
-        return loss.detach()
+        self.loss.copy_(loss.detach())
 
     def probe_step(self, clip_):
         if self.g is None or self.steps < self.warmup:
@@ -84,11 +97,13 @@ def main():
                              (self.cond, clip_.cond), (self.feats, enc)):
                 dst.copy_(src)
         self.g.replay()
+        if a.snap:
+            probe["_snap_t"] = self.loss.clone()
+            probe["_pre_t"] = self.loss_pre.clone()
         if a.sync:
             torch.cuda.synchronize()
             probe["loss_out"] = float(self.loss)
-            if a.keep_pred:
-                probe["mse_pred"] = float(F.mse_loss(self.pred, self.eps))
+            probe["mse_pred"] = float(F.mse_loss(self.pred, self.eps))
         self.tr.opt.step()
         if a.sync:
             torch.cuda.synchronize()
@@ -99,17 +114,35 @@ def main():
         return loss
 
     G._body = body
+    G.loss = torch.zeros((), dtype=torch.float32, device=dev)
+    if a.snap:
+        G.loss_pre = torch.zeros((), dtype=torch.float32, device=dev)
     report = []
+    import random
     for step in range(a.steps):
         probe.clear()
         if tw is not None:
+            if a.seed_each_step:
+                torch.manual_seed(1000 + step)
+                np.random.seed(1000 + step)
+                random.seed(1000 + step)
             le = float(tw.step(clip))
         else:
             le = None
-        if tr.graph.g is not None and (a.sync or a.keep_pred):
+        if tr.graph.g is not None and (a.sync or a.keep_pred or a.snap):
             G.step = probe_step
+        if a.seed_each_step:
+            torch.manual_seed(1000 + step)
+            np.random.seed(1000 + step)
+            random.seed(1000 + step)
         lr_ = tr.step(clip)
         G.step = orig_step
+        if a.compare_weights and twin is not None:
+            probe["n_weights_differ"] = sum(1 for pe, pg in zip(twin.parameters(), m.parameters())
+                                            if not torch.equal(pe, pg))
+        for key in ("_snap_t", "_pre_t"):
+            if key in probe:
+                probe[key[1:-2]] = float(probe.pop(key))
         rec = {"step": step, "graph": tr.graph.g is not None, "returned": float(lr_),
                "eager_twin": le, **probe}
         if tr.graph.g is not None:
