@@ -40,8 +40,16 @@ def test_bench_spawns_two_ranks_train():
     assert r["value"] > 0
 
 
-def test_bench_spawns_two_ranks_vivit_graph_ddp():
+def test_bench_spawns_two_ranks_vivit_ddp():
+    """N > 1 ViViT: eager with the bucketed all-reduce by default (advisor r03: the graph
+    form has not run over RCCL yet), graph replays around one all-reduce with
+    --vivit-graph-ddp."""
     r, _ = _run(["--only", "vivit", "--vivit-steps", "3", "--vivit-batch", "4"])
+    v = r["vivit"]
+    assert v.get("error") is None, v
+    assert v["hip_graph"] is False and v["parallelism"] == "dp2"
+    r, _ = _run(["--only", "vivit", "--vivit-steps", "3", "--vivit-batch", "4",
+                 "--vivit-graph-ddp"])
     v = r["vivit"]
     assert v.get("error") is None, v
     assert v["hip_graph"] is True and v["parallelism"] == "dp2"

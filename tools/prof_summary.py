@@ -47,6 +47,16 @@ def main(path):
               f"{mx / 1e3:.1f} | {100 * tot / total:.2f} |")
     print(f"\nTotal kernel time: {total / 1e6:.3f} ms over {sum(r[0] for r in rows.values())} "
           f"dispatches")
+    # the bench's roofline unit (the head_dim-64 backward pair at N = 262144, one sequence per
+    # launch: 8 N^2 D algorithmic FLOP) from these averages, to set beside roofline.frac
+    dq, dkdv = rows.get("vd_attn_bwd_dq_d64"), rows.get("vd_attn_bwd_dkdv_d64")
+    if dq and dkdv:
+        unit_us = dq[1] / dq[0] / 1e3 + dkdv[1] / dkdv[0] / 1e3
+        flop = 8.0 * 262144 ** 2 * 64
+        print(f"\nD = 64 backward unit from these averages: {unit_us / 1e3:.3f} ms = "
+              f"{flop / (unit_us * 1e-6) / 1e12:.1f} TFLOP/s algorithmic = "
+              f"frac {flop / (unit_us * 1e-6) / 2.5e15:.4f} of 2.5 PF/s "
+              f"(every launch of the process, warm-up and auxiliary legs included)")
 
 
 if __name__ == "__main__":
