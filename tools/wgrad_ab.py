@@ -29,7 +29,8 @@ SHAPES = ((256, 256, 3, 32, 16, 10), (64, 64, 3, 128, 16, 7), (128, 128, 3, 64, 
 def main():
     atomic = os.environ.get("VDIFF_WGRAD_ATOMIC", "0") == "1"
     tag = (f"xcd={os.environ.get('VDIFF_WGRAD_XCD', '1')} {'atomic' if atomic else 'det'}"
-           f"{' ks' if os.environ.get('VDIFF_WGRAD_KS', '0') == '1' else ''}")
+           f"{' ks' if os.environ.get('VDIFF_WGRAD_KS', '0') == '1' else ''}"
+           f"{' wide' if os.environ.get('VDIFF_WGRAD_WIDE', '0') == '1' else ''}")
     tot3 = tot1 = 0.0
     worst = 0.0
     for Ci, Co, k, H, T, per in SHAPES:
