@@ -13,7 +13,7 @@ module provides
 
 Hazard distances (gfx950; measured from hipcc's own padding of the same instruction pairs, the
 store-data rule from LLVM's hazard recognizer -- a VALU write of the data VGPRs of a VMEM store
-wider than 64 bits needs 2 wait states on gfx940+):
+wider than 64 bits needs 2 wait states between them on gfx940+):
 MFMA 32x32x16 write -> VALU / VMEM / DS / MFMA-A/B read 12 wait states (16x16x32: 8); VALU write -> MFMA
 read 2; transcendental write -> VALU read 2 (one instruction between); an MFMA reading its
 own accumulator chain as srcC needs none.  Wait states are counted as issued instructions
@@ -130,8 +130,9 @@ class Stream:
     VALU_TO_MFMA = 2   # VALU write -> MFMA read
     TRANS_RAW = 2      # transcendental write -> VALU read
     MFMA_WAR = 12      # VALU write of an in-flight MFMA's source
-    STORE_DATA = 2     # VALU write of the data VGPRs of a VMEM store wider than 64 bits
-                       # (gfx940+: 2 wait states; LLVM GCNHazardRecognizer)
+    STORE_DATA = 3     # VALU write of the data VGPRs of a VMEM store wider than 64 bits:
+                       # 2 wait states between them (gfx940+, LLVM GCNHazardRecognizer; the
+                       # distances here count the producing instruction itself)
 
     def __init__(self):
         self.lines = []

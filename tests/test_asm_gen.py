@@ -114,3 +114,53 @@ def test_d256_lane_tables(gens):
             for i in range(8):
                 seen.add((t[64 * w + lane][16 + i], t[64 * w + lane][24 + i]))
     assert len(seen) == 32 * 32
+
+
+def test_stream_hazard_padding(gens):
+    """asmgen.Stream pads the gfx950 wait-state hazards the generators rely on (round 4), as
+    wait states inserted between back-to-back instructions: a 128-bit VMEM store's data VGPRs
+    rewritten by a VALU op, 2 (LLVM's gfx940 rule; the D = 256 fp32 partial epilogues had
+    none and lost the stores of lanes 12-15 of every 16); a v_mfma_f32_16x16x32_bf16 result
+    read by VALU, 7; a 32x32x16 one, 11; a 64-bit store and an accumulator chain, none."""
+    sys.path.insert(0, ASM)
+    try:
+        from asmgen import Stream
+    finally:
+        sys.path.remove(ASM)
+
+    def nops(*lines):
+        st = Stream()
+        for ln in lines:
+            st.emit(ln)
+        return st.nops
+
+    assert nops("buffer_store_dwordx4 v[0:3], v10, s[0:3], 0 offen",
+                "v_accvgpr_read_b32 v0, a0") == 2
+    assert nops("buffer_store_dwordx4 v[0:3], v10, s[0:3], 0 offen",
+                "v_mov_b32 v9, 0", "v_accvgpr_read_b32 v0, a0") == 1
+    assert nops("buffer_store_dwordx2 v[0:1], v10, s[0:3], 0 offen",
+                "v_accvgpr_read_b32 v0, a0") == 0
+    assert nops("buffer_store_dwordx4 v[0:3], v10, s[0:3], 0 offen",
+                "v_accvgpr_read_b32 v4, a0") == 0
+    assert nops("v_mfma_f32_16x16x32_bf16 a[0:3], v[0:3], v[4:7], 0",
+                "v_accvgpr_read_b32 v8, a0") == 7
+    assert nops("v_mfma_f32_32x32x16_bf16 a[0:15], v[0:3], v[4:7], 0",
+                "v_accvgpr_read_b32 v8, a0") == 11
+    assert nops("v_mfma_f32_32x32x16_bf16 a[0:15], v[0:3], v[4:7], 0",
+                "v_mfma_f32_32x32x16_bf16 a[0:15], v[8:11], v[12:15], a[0:15]") == 0
+
+
+def test_fwd_row_sum_mfma_variant(gens):
+    """gen_fwd MSUM=2 (A/B knob, round 4): 8 v_mfma_f32_16x16x32_bf16 per body replace the
+    row-sum adds, the selector A operand is set once in the prologue, and the variant still
+    fits the register file and assembles."""
+    _, F64, *_ = gens
+    saved = F64.MSUM
+    try:
+        F64.MSUM = 2
+        k, st = F64.gen_fwd()
+    finally:
+        F64.MSUM = saved
+    text = st.text()
+    assert text.count("v_mfma_f32_16x16x32_bf16") == 8 * 16
+    assert text.count("v_add_f32") < 200  # the per-score adds are gone (l updates remain)

@@ -10,3 +10,8 @@ for w in 1 2 0; do
   rc=$?; grep -v amdgpu.ids gpurun_out/${T}_wgrad_wide$w.log | grep -E "k3|per train"
   [ $rc -eq 0 ] || { echo "rc=$rc: stopping"; tail -5 gpurun_out/${T}_wgrad_wide$w.log; exit $rc; }
 done
+# the D = 256 asm backward after the store-data padding went from 1 to 2 wait states
+timeout -k 10 300 python3 -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_attention_asm256.py > gpurun_out/${T}_asm256_tests.log 2>&1
+rc=$?; tail -1 gpurun_out/${T}_asm256_tests.log
+exit $rc
