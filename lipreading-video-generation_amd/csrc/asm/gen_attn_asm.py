@@ -485,6 +485,7 @@ def main():
     from gen_fwd import gen_fwd
     from gen_d256 import gen_dq256
     from gen_d256dk import gen_dkdv256
+    from gen_fwd256 import gen_fwd256
     kdq, ddq, sdq = gen_dq()
     kdk, ddk, sdk = gen_dkdv()
     kfw, sfw = gen_fwd()
@@ -493,14 +494,15 @@ def main():
     kfw2, dfw2, sfw2 = gen_fwd128()
     kdq4, ddq4, sdq4 = gen_dq256()
     kdk4, ddk4, sdk4 = gen_dkdv256()
+    kfw4, sfw4 = gen_fwd256()
     with open(out, "w") as f:
         f.write("// generated by gen_attn_asm.py -- do not edit\n")
-        f.write(code_object_text([kdq, kdk, kfw, kdk2, kdq2, kfw2, kdq4, kdk4],
+        f.write(code_object_text([kdq, kdk, kfw, kdk2, kdq2, kfw2, kdq4, kdk4, kfw4],
                                  ddq + ddk + ddk2 + dfw2 + ddq4 + ddk4))
     if "--report" in sys.argv:
         for name, st in (("dq", sdq), ("dkdv", sdk), ("fwd", sfw), ("dkdv128", sdk2),
                          ("dq128", sdq2), ("fwd128", sfw2), ("dq256", sdq4),
-                         ("dkdv256", sdk4)):
+                         ("dkdv256", sdk4), ("fwd256", sfw4)):
             print(f"{name}: {len(st.lines)} lines, {st.nops} nop wait states, {st.waits} lgkm "
                   f"waits, {st.forced} forced by the 15-read limit ({st.young} on young reads)")
 

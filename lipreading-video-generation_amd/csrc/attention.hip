@@ -1878,6 +1878,13 @@ const bool g_asm256 = [] {
   return !(e && atoi(e) == 0);
 }();
 
+// D = 256 hand-scheduled forward (asm/gen_fwd256.py): the default only with VDIFF_ASM256_FWD=1
+// until its parity and timing are measured on the GPU (config "asm" selects it explicitly)
+const bool g_asm256fwd = [] {
+  const char* e = getenv("VDIFF_ASM256_FWD");
+  return e && atoi(e) != 0;
+}();
+
 AttnCfg pick_cfg(int D, bool bf16, int kind) {
   const int env = g_cfg.load(std::memory_order_relaxed);
   if (!bf16) return kBase;
@@ -1900,12 +1907,13 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only
       !(env == kP4N2 && (D != 64 || kind == 0)) &&   // 2-block pipelined: D = 64 backward
       !(env == kSP && (D != 64 || kind == 0)) &&     // fragment-pipelined: D = 64 backward
-      !(env == kAsm && D != 64 && D != 128 && !(D == 256 && kind != 0)) &&  // hand-scheduled
+      !(env == kAsm && D != 64 && D != 128 && D != 256) &&  // hand-scheduled
       !(env == kRole && (D != 256 || kind != 2)))    // role-split pairs: D = 256 dK/dV
     c = (AttnCfg)env;
   else if (D == 64) c = kAsm;  // falls back to D8N / P8 off its shapes
   else if (D == 128) c = kAsm;  // asm falls back to D8N / W8 / PAIR off its shapes
   else if (D == 256 && kind != 0) c = g_asm256 ? kAsm : (kind == 2 ? kRole : kBase);
+  else if (D == 256 && kind == 0 && g_asm256fwd) c = kAsm;
   if (c == kNB2 && (D == 256 || (kind == 2 && D > 64))) c = kBase;
   if (c == kW8 && D != 64 && D != 128) c = kBase;  // 8 waves need >= 1 DMA piece each
   if (c == kP8 && D != 64) c = kP4;
@@ -1979,6 +1987,19 @@ int dq256_lsplit(const vd_attn_desc* d) {
 }
 int64_t dq256_kps(const vd_attn_desc* d, int l) {
   return vd_cdiv(vd_cdiv(d->seq_len, (int64_t)1 << l), 128) * 128;
+}
+// key splits (log2) of the hand-scheduled head_dim-256 forward: the dQ rule (128 queries per
+// workgroup, 128-key iterations, every split non-empty); attn_fwd_combine_kernel merges <= 4
+int fwd256_lsplit(const vd_attn_desc* d) {
+  const int64_t n = d->seq_len, wgs = vd_cdiv(n, 128) * d->nseq;
+  const int cap = lsplit_cap("VDIFF_ASM256_FWD_L", 2);
+  int l = 0;
+  while (l < cap && (wgs << l) < 256) {
+    const int64_t S = 2 << l, kps = vd_cdiv(vd_cdiv(n, S), 128) * 128;
+    if ((S - 1) * kps >= n) break;
+    ++l;
+  }
+  return l;
 }
 
 // query splits (log2) of the hand-scheduled head_dim-256 dK/dV (64 keys per workgroup): up to
@@ -2057,8 +2078,11 @@ int fwd_launch(const vd_attn_desc* d, KvAddr kv, const void* q, const void* k, c
 template <int D>
 size_t fwd_ws_bytes(const vd_attn_desc* d, int nkv, bool cross) {
   if (d->dtype != VD_BF16) return 0;
-  if (!cross && pick_cfg(D, true, 0) != kBase) return 0;  // only the 4-wave shape splits
-  const int s = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv);
+  int s = 1;
+  if (D == 256 && !cross && pick_cfg(D, true, 0) == kAsm)  // the asm split or the base fallback
+    s = std::max(1 << fwd256_lsplit(d), kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv));
+  else if (!cross && pick_cfg(D, true, 0) != kBase) return 0;  // only the 4-wave shape splits
+  else s = kv_splits(d, vd_cdiv(d->seq_len, 128) * d->nseq, nkv);
   return s > 1 ? (size_t)s * d->nseq * d->seq_len * (D + 2) * sizeof(float) : 0;
 }
 
@@ -2133,6 +2157,54 @@ int fwd_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const vo
   return rc ? rc : vd::check_launch("attn_fwd");
 }
 
+// hand-scheduled head_dim-256 forward (asm/gen_fwd256.py, 128 queries per workgroup) with its
+// key split into FwdSplit partials (ws: the forward workspace; too small -> no split)
+int fwd256_asm_launch(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                      void* o, float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
+  const int64_t n = d->seq_len;
+  const size_t rows = (size_t)d->nseq * n;
+  int l = fwd256_lsplit(d);
+  if (l && (!ws || ws_bytes < ((size_t)1 << l) * rows * (256 + 2) * sizeof(float))) l = 0;
+  const int64_t kps = dq256_kps(d, l);
+  vd::AsmFwd256Args a{};
+  vd::AsmFwdArgs& b = a.b;
+  b.q = q; b.k = k; b.v = v; b.o = o; b.lse = lse;
+  b.n = (uint32_t)n;
+  b.ts_bytes = (uint32_t)(d->token_stride * 2);
+  b.ots_bytes = (uint32_t)(d->o_token_stride * 2);
+  b.groups = (uint32_t)d->groups;
+  b.bs_bytes = (uint64_t)d->batch_stride * 2;
+  b.gs_bytes = (uint64_t)d->group_stride * 2;
+  b.obs_bytes = (uint64_t)d->o_batch_stride * 2;
+  b.ogs_bytes = (uint64_t)d->o_group_stride * 2;
+  b.qscale = d->scale * kLog2e;
+  b.kv_bytes = (uint32_t)(((n - 1) * d->token_stride + 256) * 2);
+  b.o_bytes = (uint32_t)(((n - 1) * d->o_token_stride + 256) * 2);
+  b.tile_bytes = (uint32_t)(32 * d->token_stride * 2);
+  float* part = l ? (float*)ws : nullptr;
+  a.part = part;
+  a.kps = (uint32_t)kps;
+  a.lsplit = (uint32_t)l;
+  a.split_bytes = (uint64_t)rows * 1024;
+  a.ml_off = ((uint64_t)1 << l) * rows * 1024;
+  a.ml_split_bytes = (uint32_t)(rows * 8);
+  const unsigned gy = (unsigned)d->groups, gz = (unsigned)(d->nseq / d->groups) << l;
+  int rc = vd::asm_fwd_d256(a, (unsigned)vd_cdiv(n, 128), gy, gz, st);
+  if (rc) return rc;
+  if (l) {
+    rc = vd::check_launch("attn_fwd");
+    if (rc) return rc;
+    const SeqAddr oa{d->o_batch_stride, d->o_group_stride, d->groups};
+    const int64_t work = (int64_t)rows * (256 / 8);
+    int g = (int)vd_cdiv(work, 256);
+    if (g > 4096) g = 4096;
+    attn_fwd_combine_kernel<bf16_t, 256><<<g, 256, 0, st>>>(part, 1 << l, d->nseq, (int)n,
+                                                           (bf16_t*)o, oa, d->o_token_stride,
+                                                           lse);
+  }
+  return vd::check_launch("attn_fwd");
+}
+
 template <typename T, int D>
 int fwd_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const void* k,
              const void* v, void* o, float* lse, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -2154,6 +2226,9 @@ int fwd_impl(const vd_attn_desc* d, KvAddr kv, bool cross, const void* q, const 
     if constexpr (D == 128)
       if (c == kAsm && asm_fwd_ok(d, q, k, v, o, lse, D))
         return fwd_asm_launch(d, q, k, v, o, lse, st);
+    if constexpr (D == 256)
+      if (c == kAsm && asm_fwd_ok(d, q, k, v, o, lse, D))
+        return fwd256_asm_launch(d, q, k, v, o, lse, ws, ws_bytes, st);
     if constexpr (D == 128)
       if (c == kD8N || c == kAsm) return fwd_defer_launch<T, D, 8, false>(d, q, k, v, o, lse, st);
     if constexpr (D == 64 || D == 128)  // the pipelined forward is retired: its successor

@@ -112,4 +112,23 @@ static_assert(sizeof(AsmDkdv256Args) == 176, "kernarg block layout");
 int asm_bwd_dkdv_d256(const AsmDkdv256Args& a, unsigned gx, unsigned gy, unsigned gz,
                       hipStream_t stream);
 
+// vd_attn_fwd_d256 (asm/gen_fwd256.py): the forward block plus the key split -- split z of
+// 2^lsplit takes keys [z kps, min(n, (z + 1) kps)) and, with part != 0, writes its
+// unnormalised O (fp32, part + z split_bytes: [seq][n][256]) and (m in log2 units, l) rows
+// (part + ml_off + z ml_split_bytes: [seq][n][2]) in attention.hip's FwdSplit layout for
+// attn_fwd_combine_kernel.  b.niter / b.klim0 are unused (the kernel derives its iterations
+// from its split's key count).  grid (ceil(n / 128), groups, (nseq / groups) << lsplit), 256
+// threads, 128 KiB static LDS
+struct AsmFwd256Args {
+  AsmFwdArgs b;
+  float* part;
+  uint32_t kps, lsplit;
+  uint64_t split_bytes;
+  uint64_t ml_off;
+  uint32_t ml_split_bytes, pad[3];
+};
+static_assert(sizeof(AsmFwd256Args) == 160, "kernarg block layout");
+int asm_fwd_d256(const AsmFwd256Args& a, unsigned gx, unsigned gy, unsigned gz,
+                 hipStream_t stream);
+
 }  // namespace vd

@@ -38,7 +38,7 @@ def test_code_object_assembles(tmp_path, gens):
     text = out.read_text()
     for name in ("vd_attn_bwd_dq_d64", "vd_attn_bwd_dkdv_d64", "vd_attn_fwd_d64",
                  "vd_attn_bwd_dkdv_d128", "vd_attn_bwd_dq_d128", "vd_attn_fwd_d128",
-                 "vd_attn_bwd_dq_d256", "vd_attn_bwd_dkdv_d256"):
+                 "vd_attn_bwd_dq_d256", "vd_attn_bwd_dkdv_d256", "vd_attn_fwd_d256"):
         assert f".amdhsa_kernel {name}" in text, name
     subprocess.run([CLANG, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
                     "-c", str(out), "-o", str(tmp_path / "a.o")], check=True)
@@ -93,6 +93,24 @@ def test_instruction_mix_per_tile(gens):
     c = _body_counts(st.lines, "B: query tile, ring stage 1", "B: query tile, ring stage 2")
     assert c[mf] == 32 and c["v_mul_f32"] == 16 and c["ds_read_b128"] == 16 + 4 + 4
     assert c.get("s_nop", 0) <= 20
+
+
+def test_fwd256_body(gens):
+    """vd_attn_fwd_d256 (round 4): per 32-key tile 16 S + 16 PV MFMAs, the 16 exp / 8 cvt of
+    the lagged softmax, 16 K row and 32 V^T transposed fragment reads, 8 LDS-DMA pieces, one
+    rare-path call site; registers within one wave per SIMD; the 4 rare-path entry points."""
+    import gen_fwd256 as F256
+    V, A = F256.regs()
+    assert V.next <= 256 and A.next <= 256 and (V.next + 3) // 4 * 4 + A.next <= 512
+    k, st = F256.gen_fwd256()
+    mf = "v_mfma_f32_32x32x16_bf16"
+    c = _body_counts(st.lines, "key tile, ring stage 1", "key tile, ring stage 2")
+    assert c[mf] == 32 and c["v_exp_f32"] == 16 and c["v_cvt_pk_bf16_f32"] == 8
+    assert c["ds_read_b128"] == 16 and c["ds_read_b64_tr_b16"] == 32
+    assert c["buffer_load_dwordx4"] == 8 and c["s_swappc_b64"] == 1
+    assert c.get("s_nop", 0) <= 16
+    for v in range(4):
+        assert f".Lfwd256_rare{v}:" in k[0]
 
 
 def test_d256_lane_tables(gens):

@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 T=${1:-r04p}
 timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_attention_asm256.py -k "fwd" > gpurun_out/${T}_fwd256_tests.log 2>&1
+  tests/test_gpu_attention_asm256.py -k "fwd" -rP > gpurun_out/${T}_fwd256_tests.log 2>&1
 rc=$?; grep -E "passed|failed|Error|error" gpurun_out/${T}_fwd256_tests.log | tail -5
 [ $rc -eq 0 ] || { echo "tests rc=$rc: stopping"; grep -E "rel-L2|assert" gpurun_out/${T}_fwd256_tests.log | tail -20; exit $rc; }
 timeout -k 10 200 python3 -u tools/fwd256_ab.py > gpurun_out/${T}_fwd256_ab.log 2>&1
