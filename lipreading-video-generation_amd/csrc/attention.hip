@@ -1878,11 +1878,12 @@ const bool g_asm256 = [] {
   return !(e && atoi(e) == 0);
 }();
 
-// D = 256 hand-scheduled forward (asm/gen_fwd256.py): the default only with VDIFF_ASM256_FWD=1
-// until its parity and timing are measured on the GPU (config "asm" selects it explicitly)
+// D = 256 hand-scheduled forward (asm/gen_fwd256.py) as the default (round 4;
+// VDIFF_ASM256_FWD=0 restores the compiled 4-wave forward): 364-406 -> 240-242 us at
+// N = 16384 on one box (tools/fwd256_ab.py, profiles/r04p_fwd256_ab.txt)
 const bool g_asm256fwd = [] {
   const char* e = getenv("VDIFF_ASM256_FWD");
-  return e && atoi(e) != 0;
+  return !(e && atoi(e) == 0);
 }();
 
 AttnCfg pick_cfg(int D, bool bf16, int kind) {
@@ -1901,7 +1902,8 @@ AttnCfg pick_cfg(int D, bool bf16, int kind) {
   //            PAIR 3.97-3.99 ms on the same box (tools/gpu_asm128.sh); forward 1.67-1.68 vs
   //            D8N 2.04-2.05 ms (tools/gpu_r03c.sh)
   //   D = 256 backward (round 4): hand-scheduled dQ 0.339 / dK/dV 0.458 ms vs base 0.506 /
-  //            ROLE 0.804 ms (tools/gpu_r04f.sh)
+  //            ROLE 0.804 ms (tools/gpu_r04f.sh); forward 0.240 vs base 0.364-0.406 ms
+  //            (tools/fwd256_ab.py)
   if (env >= 0 && !((env == kD8 || env == kD8N || env == kD4) &&
                     ((D != 64 && !(D == 128 && env == kD8N)) || kind != 0)) &&
       !(env == kPair && (D != 128 || kind != 2)) &&  // the paired kernel: D = 128 dK/dV only

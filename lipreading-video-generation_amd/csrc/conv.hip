@@ -2326,6 +2326,12 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     int64_t splits = vd_cdiv(wide ? (wwide == 2 ? 256 : 512) : 2048, tiles);
     int64_t maxs = vd_cdiv(g.M, (one || plane || wide) ? 1024 : 64 * w3_msteps);
     if (splits > maxs) splits = maxs;
+    // diagnostic (tools/wgrad_splits.py): VDIFF_WGRAD_SPLITS=s forces s pixel splits
+    static const int wsplits = [] {
+      const char* e = getenv("VDIFF_WGRAD_SPLITS");
+      return e ? atoi(e) : 0;
+    }();
+    if (wsplits > 0) splits = std::min<int64_t>(wsplits, vd_cdiv(g.M, 64));
     if (splits < 1) splits = 1;
     g.m_per_split = vd_cdiv(vd_cdiv(g.M, splits), 64) * 64;
     splits = vd_cdiv(g.M, g.m_per_split);

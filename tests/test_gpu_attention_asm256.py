@@ -4,8 +4,9 @@ round 4 unless VDIFF_ASM256=0) against the compiler-scheduled kernels that run t
 order -- dQ: the 4-wave kernel (config "base": the same 32-key blocks, key split into fp32
 partials and partial sum); dK / dV: the role-split wave pairs (config "role") -- and a
 materialised fp32 reference of QKVAttentionLegacy's backward (unet.py:349-366 at C = 256, the
-32x32 level of the config-2 UNet3D).  The forward is the compiled kernel in every run here.
-Shapes: whole and ragged tiles, a batch of two sequences, the spatial grouping (groups on
+32x32 level of the config-2 UNet3D).  The backward tests' forward is the default one (the
+hand-scheduled vd_attn_fwd_d256 since round 4, tested on its own below against the compiled
+4-wave forward and an fp32 reference).  Shapes: whole and ragged tiles, a batch of two sequences, the spatial grouping (groups on
 grid.y), the config-2 length 16384 and 16384 + 17; the kernels take N >= 1024."""
 import math
 import os
@@ -172,3 +173,13 @@ def test_asm256_fwd_spatial_groups_and_fp32_reference():
     # compiled kernels (RowFrag::scale): ~2^-9 relative per score, 2.5e-3 in lse here (batch
     # r04p); the compiled kernel agrees with the asm one to 1e-4 (test above)
     assert float((l1 - torch.logsumexp(s, -1)).abs().max()) <= 1e-2
+
+
+@pytest.mark.skipif(os.environ.get("VDIFF_ASM256_FWD") == "0", reason="compiled forward selected")
+def test_asm256_fwd_is_the_d256_default():
+    from vdiff import ops
+    gen = torch.Generator(device=dev).manual_seed(29)
+    qkv = ops.to_cl((torch.randn((1, 3 * C, 2048), generator=gen, device=dev)).bfloat16())
+    o0, (l0,) = _fwd(qkv, "auto")
+    o1, (l1,) = _fwd(qkv, "asm")
+    assert torch.equal(o0, o1) and torch.equal(l0, l1)

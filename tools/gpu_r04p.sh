@@ -11,4 +11,10 @@ rc=$?; grep -E "passed|failed|Error|error" gpurun_out/${T}_fwd256_tests.log | ta
 [ $rc -eq 0 ] || { echo "tests rc=$rc: stopping"; grep -E "rel-L2|assert" gpurun_out/${T}_fwd256_tests.log | tail -20; exit $rc; }
 timeout -k 10 200 python3 -u tools/fwd256_ab.py > gpurun_out/${T}_fwd256_ab.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/${T}_fwd256_ab.log
+[ $rc -eq 0 ] || exit $rc
+# generator variants: LDS read distances ahead of the MFMAs
+timeout -k 10 300 python3 -u tools/asm_ab256.py 'base:' 'rd3:RD_AHEAD=3' 'rd4:RD_AHEAD=4' \
+  'rd5:RD_AHEAD=5' 'tr3:TR_AHEAD=3' 'tr6:TR_AHEAD=6' 'rd4tr6:RD_AHEAD=4,TR_AHEAD=6' 'ch1:CHAINS=1' \
+  'base2:' > gpurun_out/${T}_asm_ab256.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/${T}_asm_ab256.log
 exit $rc
