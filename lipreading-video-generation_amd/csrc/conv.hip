@@ -2326,6 +2326,38 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     int64_t splits = vd_cdiv(wide ? (wwide == 2 ? 256 : 512) : 2048, tiles);
     int64_t maxs = vd_cdiv(g.M, (one || plane || wide) ? 1024 : 64 * w3_msteps);
     if (splits > maxs) splits = maxs;
+    // occupancy rounds (default since round 4; VDIFF_WGRAD_QRULE=0 turns it off, =c applies
+    // it only where the rule above gives at most c splits): the grid of equal-length
+    // workgroups runs in ceil(r) rounds of the resident slots (r = workgroups / slots), so
+    // r = 1.5 pays for 2; take the fewest splits (down to a third) whose r >= 0.9 fills its
+    // last round to >= 93 %, else the best fill (profiles/r04r_wgrad_split_sweep.txt: e.g.
+    // 384->128 on 16x64x64 7 splits 217 us, 8 splits 263, the rule's 19 241).  The step's
+    // weight gradients 5.81-5.93 -> 5.47-5.48 ms (profiles/r04u_ab_wgrad_qrule.txt)
+    static const int wq = [] {
+      const char* e = getenv("VDIFF_WGRAD_QRULE");
+      return e ? atoi(e) : (1 << 30);
+    }();
+    if (wq > 0 && splits <= wq && !wide && !plane && !wks) {
+      // resident workgroups per CU: LDS ring (160 KiB per CU) and registers (3 per CU for
+      // the kw strip's 134-136 VGPRs)
+      const int nst = one ? (cot >= 128 ? (w1_nst >= 4 ? 4 : 2)
+                                        : (w1_nst >= 6 ? 6 : w1_nst >= 4 ? 4 : 2))
+                          : (w3_nst >= 3 ? 3 : 2);
+      const int ring = nst * (cot + (one ? 64 : (rows <= 96 ? 96 : rows <= 128 ? 128 : 192))) * 128;
+      const int64_t slots = 256 * (int64_t)std::max(1, std::min(3, 163840 / ring));
+      int64_t pick = 0, fill_pick = 0;
+      double best_fill = -1.0;
+      for (int64_t s = std::max<int64_t>(1, splits / 3); s <= splits; ++s) {
+        const int64_t sr = vd_cdiv(g.M, vd_cdiv(vd_cdiv(g.M, s), 64) * 64);
+        const double r = (double)(tiles * sr) / (double)slots;
+        if (r < 0.9) continue;
+        const double fill = r / std::ceil(r);
+        if (fill >= 0.93) { pick = s; break; }
+        if (fill > best_fill + 1e-9) { best_fill = fill; fill_pick = s; }
+      }
+      if (!pick) pick = fill_pick;
+      if (pick) splits = pick;
+    }
     // diagnostic (tools/wgrad_splits.py): VDIFF_WGRAD_SPLITS=s forces s pixel splits
     static const int wsplits = [] {
       const char* e = getenv("VDIFF_WGRAD_SPLITS");
