@@ -2288,14 +2288,26 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
                                              : (w1 % 1000 == 128 && d->Co % 128 == 0 ? 128 : 64);
     // 3x3(x3) kw-strip (A/B knob VDIFF_WGRAD3=nst,cot): ring depth and 64 / 128 output
     // channels per workgroup
+    // cot 0 (the default): 128 output channels per workgroup where Co % 128 == 0 and that
+    // grid can still fill 90 % of the chip's resident slots (2 workgroups per CU at 128, the
+    // ring being 2 x (128 + RW) rows), else 64 -- under the occupancy-round split rule below
+    // 128-wide tiles won on 9 of the step's 11 such shapes, losing only where the grid stays
+    // under one round (128->256 on 16x32x32, 64->128 on 16x64x64): the step's 3x3x3 weight
+    // gradients 4.75 -> 4.46 ms (profiles/r04v_ab_wgrad3_cot.txt)
     static const int w3 = [] {  // nst,cot[,pixels per split / 64]
       const char* e = getenv("VDIFF_WGRAD3");
-      int n = 2, c = 64, m = 32;
+      int n = 2, c = 0, m = 32;
       if (e) sscanf(e, "%d,%d,%d", &n, &c, &m);
       return m * 1000000 + n * 1000 + c;
     }();
     const int w3_nst = w3 / 1000 % 1000, w3_msteps = w3 / 1000000;
-    const int w3_cot = (w3 % 1000 == 128 && d->Co % 128 == 0) ? 128 : 64;
+    const int w3_c = w3 % 1000;
+    const int w3_rw = rows <= 96 ? 96 : rows <= 128 ? 128 : 192;
+    const bool w3_fill128 =
+        (int64_t)vd_cdiv(d->Co, 128) * vd_cdiv(d->Ci, 64) * d->kt * d->kh *
+            vd_cdiv(g.M, 64 * (int64_t)w3_msteps) * 10 >=
+        9 * 256 * (int64_t)std::max(1, std::min(3, 163840 / ((w3_nst >= 3 ? 3 : 2) * (128 + w3_rw) * 128)));
+    const int w3_cot = d->Co % 128 == 0 && (w3_c == 128 || (w3_c == 0 && w3_fill128)) ? 128 : 64;
     const int cot = one ? w1_cot : w3_cot;
     // nine-tap planes (VDIFF_CONV_WPLANE=1, A/B): image rows of whole 64-pixel steps
     static const int wplane = [] {
