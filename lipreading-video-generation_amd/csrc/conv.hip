@@ -2276,11 +2276,13 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     const int rows = one ? 64 : (64 / wc) * (wc + 2);
     // 1x1 (A/B knob VDIFF_WGRAD1=nst,cot): ring depth 2 / 4 / 6 and 64 / 128 / 192 output
     // channels per workgroup (192: X read once per 192 channels of the qkv projections).
-    // Default 4,128: the train step's 1x1 weight gradients 0.864 -> 0.722 ms on one box
-    // (tools/wgrad1x1_bench.py, profiles/r03_ab_wgrad1x1.txt)
+    // Default 4,64 since the occupancy-round split rule (round 4: 0.667 -> 0.622 ms per step,
+    // the 256->768 / 256->256 / 128->128 shapes 9-19 % faster, the rest equal;
+    // profiles/r04x_ab_wgrad_knobs.txt); round 3 had measured 4,128 best under the old split
+    // rule (0.864 -> 0.722 ms, profiles/r03_ab_wgrad1x1.txt)
     static const int w1 = [] {
       const char* e = getenv("VDIFF_WGRAD1");
-      int n = 4, c = 128;
+      int n = 4, c = 64;
       if (e) sscanf(e, "%d,%d", &n, &c);
       return n * 1000 + c;
     }();
