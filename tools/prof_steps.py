@@ -9,10 +9,14 @@ from prof_summary import short  # noqa: E402
 
 
 def cat(n):
-    if n.startswith("attn_"):
+    if n.startswith(("attn_", "vd_attn_")):
         return "attention (vdiff)"
-    if n.startswith(("igemm_dma", "wgrad_dma", "pw_gemm", "igemm_bf16", "conv_gemm", "pack_weight",
-                     "channel_sums", "conv_wgrad")):
+    if n.startswith(("wgrad_dma", "wgrad_finish", "conv_wgrad")):
+        return "conv weight gradient (vdiff)"
+    if n.startswith("channel_sums"):
+        return "conv bias / emb-add gradient (vdiff)"
+    if n.startswith(("igemm_dma", "pw_gemm", "igemm_bf16", "conv_gemm", "pack_weight",
+                     "halo_conv")):
         return "conv (vdiff)"
     if n.startswith("gn_"):
         return "groupnorm (vdiff)"
