@@ -211,3 +211,30 @@ def test_conv_wgrad_fixed_order_config2(shape, Co, k):
     ref = torch.nn.grad.conv3d_weight(x.float().cpu().contiguous(), w.shape,
                                       dy.float().cpu().contiguous(), padding=pad)
     assert rel_l2(a, ref) < 1e-4, rel_l2(a, ref)
+
+
+@pytest.mark.parametrize("shape,Co,k", [((1, 128, 16, 64, 64), 128, 3),    # 128-wide kw-strip tiles
+                                       ((1, 384, 16, 64, 64), 128, 3),
+                                       ((1, 512, 16, 32, 32), 256, 3),
+                                       ((1, 128, 16, 32, 32), 256, 3),    # 64-wide (grid < a round)
+                                       ((2, 128, 8, 64, 64), 128, 3),     # two clips
+                                       ((1, 64, 16, 128, 128), 3, 3),     # the 64->3 output conv
+                                       ((1, 256, 1, 128, 128), 768, 1),   # qkv 1x1, 64-wide tiles
+                                       ((1, 200, 16, 64, 64), 64, 3)])    # padded Ci
+def test_conv_wgrad_round4_split_rule(shape, Co, k):
+    """The round-4 weight-gradient launch choices (occupancy-round pixel splits, 128-wide
+    kw-strip tiles where their grid fills the chip, 64-wide 1x1 tiles): bit-identical run to
+    run and within fp32 summation order of the fp32 parity-mode weight gradient
+    (conv_wgrad_kernel<float>, exact-fp32 MFMA, itself checked against the oracle and torch
+    above) of the same bf16 values."""
+    from vdiff import ops
+    x = ops.to_cl(seeded(shape, 17).to(dev, torch.bfloat16))
+    w = (seeded((Co, shape[1]) + (k,) * 3, 18) / (shape[1] * k ** 3) ** 0.5).to(dev)
+    pad = k // 2
+    y = ops.conv(x, w, None, padding=pad)
+    dy = ops.to_cl(seeded(tuple(y.shape), 19).to(dev, torch.bfloat16))
+    a = _wgrad(x, w, dy, 1, pad, False)
+    b = _wgrad(x, w, dy, 1, pad, False)
+    assert torch.equal(a, b)
+    ref = _wgrad(ops.to_cl(x.float()), w, ops.to_cl(dy.float()), 1, pad, False)
+    assert rel_l2(a, ref) < 1e-5, rel_l2(a, ref)
