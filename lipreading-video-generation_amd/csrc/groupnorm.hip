@@ -15,8 +15,18 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kVec = 8;             // channels per lane
-constexpr int kTargetChunks = 2048; // workgroups per launch (B * nchunk)
-constexpr int kSumPer = 64;         // chunk partials per gn_bwd_sum_kernel workgroup
+// workgroups per launch (B * nchunk) and chunk partials per gn_bwd_sum_kernel workgroup;
+// VDIFF_GN_CHUNKS / VDIFF_GN_SUMPER override them for A/B runs (read once per process).
+// 1024 (round 4; 2048 before): the forward 7-10 us faster on 8 of the step's 9 shapes (half
+// the chunk partials for the finalize pass), the backward 2-6 us on 7 of 9, +4 us on C = 192
+// at 16x128x128 (tools/gn_bench.py --capi, profiles/r04ad_ab_gn_chunks.txt)
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+const int kTargetChunks = env_int("VDIFF_GN_CHUNKS", 1024);
+const int kSumPer = env_int("VDIFF_GN_SUMPER", 64);
 
 struct GNPlan {
   int rows_per_iter;  // pixel rows a WG covers per iteration
@@ -315,6 +325,7 @@ __global__ void gn_bwd_finalize_kernel(float* __restrict__ sums, int ksplit, int
   const int64_t slice = (int64_t)B * C * 2;
   for (int i = threadIdx.x; i < B * C; i += blockDim.x) {
     float a = sums[2 * i], s = sums[2 * i + 1];
+#pragma unroll 8
     for (int z = 1; z < ksplit; ++z) {
       a += sums[z * slice + 2 * i];
       s += sums[z * slice + 2 * i + 1];

@@ -29,7 +29,42 @@ def timeit(fn, reps=20):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
+def capi(C, T, H, reps=50):
+    """GPU time of the C-ABI calls alone (back to back, no autograd): fwd, bwd in us."""
+    from vdiff import _lib
+    B, S, G = 1, T * H * H, 32
+    x = torch.randn(B, S, C, device="cuda").bfloat16()
+    dy = torch.randn(B, S, C, device="cuda").bfloat16()
+    y, dx = torch.empty_like(x), torch.empty_like(x)
+    g32 = torch.randn(C, device="cuda")
+    b32 = torch.randn(C, device="cuda")
+    mean = torch.empty(B * G, device="cuda")
+    rstd = torch.empty_like(mean)
+    dg, db = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    ws = torch.empty(_lib.lib().vd_groupnorm_workspace_size(B, S, C, G), dtype=torch.uint8,
+                     device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    dt = ops._DT[torch.bfloat16]
+    p = lambda t: t.data_ptr()  # noqa: E731
+
+    def fwd():
+        _lib.call("vd_groupnorm_silu_fwd", p(x), p(g32), p(b32), p(y), p(mean), p(rstd), B, S, C,
+                  G, 1e-5, 1, 0.0, 0, dt, p(ws), st)
+
+    def bwd():
+        _lib.call("vd_groupnorm_silu_bwd", p(x), p(dy), p(g32), p(b32), p(mean), p(rstd), p(dx),
+                  p(dg), p(db), B, S, C, G, 1, 0.0, 0, dt, p(ws), st)
+    return timeit(fwd, reps), timeit(bwd, reps)
+
+
 def main():
+    if "--capi" in sys.argv:
+        for C, T, H in SHAPES:
+            f, b = capi(C, T, H)
+            size = C * T * H * H * 2
+            print(f"GN+SiLU C-ABI C={C:4d} {T}x{H}x{H}: fwd {f:7.1f} us ({3 * size / f / 1e3:6.0f} "
+                  f"GB/s)  bwd {b:7.1f} us ({5 * size / b / 1e3:6.0f} GB/s)", flush=True)
+        return
     for C, T, H in SHAPES:
         x = ops.to_cl(torch.randn(1, C, T, H, H, device="cuda").bfloat16()).requires_grad_(True)
         w = torch.randn(C, device="cuda", requires_grad=True)
