@@ -259,9 +259,20 @@ __global__ void upsample_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx
 // block owns a run of rows of one sample, each thread sums 8 channels over its rows in fp32,
 // the block reduces through LDS and stores its partial row part[b][blk][C].  Stage 2 sums
 // the partial rows per channel (deterministic; no same-address atomics, which serialise).
-constexpr int kSumBlocks = 256;  // stage-1 blocks per sample (max)
+constexpr int kSumBlocks = 1024;  // stage-1 blocks per sample (upper bound: finish registers)
+// stage-1 blocks per sample actually launched (default 256; VDIFF_CSUM_BLOCKS, <= kSumBlocks,
+// for A/B runs) and the rows each stage-1 thread keeps in flight (VDIFF_CSUM_UNROLL 1 or 4;
+// default 4 since round 4: the step's sums 1.10 -> 0.73 ms, e.g. 192 x 262144 36.3 -> 19.4 us
+// at 5.2 TB/s, bit-identical (same add order); profiles/r04af_ab_channel_sums.txt)
+static int csum_env(const char* name, int dflt, int lo, int hi) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : dflt;
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+const int g_csum_blocks = csum_env("VDIFF_CSUM_BLOCKS", 256, 1, kSumBlocks);
+const int g_csum_unroll = csum_env("VDIFF_CSUM_UNROLL", 4, 1, 4);
 
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(256) void channel_sums_kernel(const T* __restrict__ x, int64_t S,
                                                            int C, int cs, int64_t rows_per_blk,
                                                            float* __restrict__ part) {
@@ -277,7 +288,19 @@ __global__ __launch_bounds__(256) void channel_sums_kernel(const T* __restrict__
   if (r1 > S) r1 = S;
   if (lr < rpi) {
     const T* base = x + (int64_t)b * S * cs + c8;
-    for (int64_t r = r0 + lr; r < r1; r += rpi) {
+    int64_t r = r0 + lr;
+    if constexpr (U > 1) {  // U rows' loads in flight before their adds (same add order)
+      for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+        float v[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load8(base + (r + u * rpi) * cs, v[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += v[u][e];
+      }
+    }
+    for (; r < r1; r += rpi) {
       float v[8];
       load8(base + r * cs, v);
 #pragma unroll
@@ -298,7 +321,7 @@ __global__ __launch_bounds__(256) void channel_sums_kernel(const T* __restrict__
 }
 
 // 32 channels per block, 32 row lanes per channel: at most 8 independent partial loads per
-// lane (kSumBlocks = 256), all in flight before the adds; fixed-order LDS reduce
+// lane (kSumBlocks = 1024 / 32), all in flight before the adds; fixed-order LDS reduce
 __global__ __launch_bounds__(1024) void channel_sums_finish_kernel(const float* __restrict__ part,
                                                                    int nblk, int C,
                                                                    float* __restrict__ out) {
@@ -503,7 +526,7 @@ int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dty
   hipStream_t st = VD_STREAM(stream);
   // about kSumBlocks blocks per sample, at least 4 row iterations each
   const int64_t rpi = 256 / (C / 8);
-  int64_t blocks = kSumBlocks;
+  int64_t blocks = g_csum_blocks;
   int64_t maxb = vd_cdiv(S, rpi * 4);
   if (blocks > maxb) blocks = maxb;
   if (blocks < 1) blocks = 1;
@@ -511,8 +534,12 @@ int vd_channel_sums(const void* x, int B, int64_t S, int C, int cstride, int dty
   blocks = vd_cdiv(S, rows);
   float* part = reinterpret_cast<float*>(workspace);
   return VD_DISPATCH_DTYPE(dtype, Tp, {
-    channel_sums_kernel<Tp><<<dim3((unsigned)blocks, (unsigned)B), 256, 0, st>>>(
-        (const Tp*)x, S, C, cs, rows, part);
+    if (g_csum_unroll >= 4)
+      channel_sums_kernel<Tp, 4><<<dim3((unsigned)blocks, (unsigned)B), 256, 0, st>>>(
+          (const Tp*)x, S, C, cs, rows, part);
+    else
+      channel_sums_kernel<Tp, 1><<<dim3((unsigned)blocks, (unsigned)B), 256, 0, st>>>(
+          (const Tp*)x, S, C, cs, rows, part);
     channel_sums_finish_kernel<<<dim3((unsigned)vd_cdiv(C, 32), (unsigned)B), 1024, 0, st>>>(
         part, (int)blocks, C, out);
   });
