@@ -27,6 +27,9 @@ static int env_int(const char* name, int dflt) {
 }
 const int kTargetChunks = env_int("VDIFF_GN_CHUNKS", 1024);
 const int kSumPer = env_int("VDIFF_GN_SUMPER", 64);
+// pixel rows whose loads each thread keeps in flight before using them (VDIFF_GN_UNROLL 1, 2, 4;
+// the per-row arithmetic and the accumulation order are unchanged)
+const int kUnroll = env_int("VDIFF_GN_UNROLL", 1) >= 4 ? 4 : (env_int("VDIFF_GN_UNROLL", 1) >= 2 ? 2 : 1);
 
 struct GNPlan {
   int rows_per_iter;  // pixel rows a WG covers per iteration
@@ -85,7 +88,7 @@ static const uint64_t* g_drop_ctr = nullptr;  // vd_set_dropout_counter
 
 // ---------------------------------------------------------------- forward
 // grid (nchunk, B).  Per WG: per-group (n, mean, M2) over its chunk.
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(kThreads) void gn_stats_kernel(const T* __restrict__ x, int64_t S,
                                                             int C, int G, int64_t chunk_px,
                                                             int rows_per_iter,
@@ -107,7 +110,25 @@ __global__ __launch_bounds__(kThreads) void gn_stats_kernel(const T* __restrict_
   for (int j = 0; j < kVec; ++j) s1[j] = s2[j] = shift[j] = 0.f;
   if (active && p0 + r < p1) load8(xb + (p0 + r) * C + cv * kVec, shift);
   if (active) {
-    for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
+    int64_t p = p0 + r;
+    if constexpr (U > 1) {
+      for (; p + (U - 1) * rows_per_iter < p1; p += U * rows_per_iter) {
+        float v[U][kVec];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load8(xb + (p + u * rows_per_iter) * C + cv * kVec, v[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int j = 0; j < kVec; ++j) {
+            const float d = v[u][j] - shift[j];
+            s1[j] += d;
+            s2[j] += d * d;
+          }
+          cnt += 1.f;
+        }
+      }
+    }
+    for (; p < p1; p += rows_per_iter) {
       float v[kVec];
       load8(xb + p * C + cv * kVec, v);
 #pragma unroll
@@ -179,7 +200,7 @@ __global__ __launch_bounds__(kThreads) void gn_finalize_kernel(const float* __re
 // grid (nchunk, B): each thread keeps one 8-channel vector for all its pixel rows, so the
 // per-channel scale/shift (gamma * rstd, beta - mean * gamma * rstd) is computed once and
 // the loop is one FMA (+ SiLU, dropout) per element -- no index division per element.
-template <typename T, bool SILU>
+template <typename T, bool SILU, int U>
 __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict__ x,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
@@ -203,7 +224,26 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict_
   const int64_t p0 = (int64_t)blockIdx.x * chunk_px;
   int64_t p1 = p0 + chunk_px;
   if (p1 > S) p1 = S;
-  for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
+  int64_t p = p0 + r;
+  if constexpr (U > 1) {
+    for (; p + (U - 1) * rows_per_iter < p1; p += U * rows_per_iter) {
+      float v[U][kVec];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        load8(x + ((int64_t)b * S + p + u * rows_per_iter) * C + cv * kVec, v[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e0 = ((int64_t)b * S + p + u * rows_per_iter) * C + cv * kVec;
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+          const float z = v[u][j] * sc[j] + sh[j];
+          v[u][j] = (SILU ? silu_f(z) : z) * drop.mul(e0 + j);
+        }
+        store8(y + e0, v[u]);
+      }
+    }
+  }
+  for (; p < p1; p += rows_per_iter) {
     const int64_t e0 = ((int64_t)b * S + p) * C + cv * kVec;
     float v[kVec];
     load8(x + e0, v);
@@ -218,7 +258,7 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const T* __restrict_
 
 // ---------------------------------------------------------------- backward
 // grid (nchunk, B): per-channel partial sums A = sum dz, Bs = sum dz * xhat
-template <typename T, bool SILU>
+template <typename T, bool SILU, int U>
 __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -248,10 +288,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
       be[j] = beta[c];
       sa[j] = sb[j] = 0.f;
     }
-    for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
-      float v[kVec], d[kVec];
-      load8(xb + p * C + cv * kVec, v);
-      load8(db + p * C + cv * kVec, d);
+    auto row = [&](int64_t p, const float* v, const float* d) {
 #pragma unroll
       for (int j = 0; j < kVec; ++j) {
         const float xh = (v[j] - mu[j]) * rs[j];
@@ -264,6 +301,25 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_reduce_kernel(
         sa[j] += dz;
         sb[j] += dz * xh;
       }
+    };
+    int64_t p = p0 + r;
+    if constexpr (U > 1) {
+      for (; p + (U - 1) * rows_per_iter < p1; p += U * rows_per_iter) {
+        float v[U][kVec], d[U][kVec];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          load8(xb + (p + u * rows_per_iter) * C + cv * kVec, v[u]);
+          load8(db + (p + u * rows_per_iter) * C + cv * kVec, d[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) row(p + u * rows_per_iter, v[u], d[u]);
+      }
+    }
+    for (; p < p1; p += rows_per_iter) {
+      float v[kVec], d[kVec];
+      load8(xb + p * C + cv * kVec, v);
+      load8(db + p * C + cv * kVec, d);
+      row(p, v, d);
     }
 #pragma unroll
     for (int j = 0; j < kVec; ++j) sh[r * C + cv * kVec + j] = make_float2(sa[j], sb[j]);
@@ -359,7 +415,7 @@ __global__ void gn_bwd_finalize_kernel(float* __restrict__ sums, int ksplit, int
 }
 
 // grid (nchunk, B), per-thread channel constants as gn_apply_kernel
-template <typename T, bool SILU>
+template <typename T, bool SILU, int U>
 __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -384,11 +440,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
   const int64_t p0 = (int64_t)blockIdx.x * chunk_px;
   int64_t p1 = p0 + chunk_px;
   if (p1 > S) p1 = S;
-  for (int64_t p = p0 + r; p < p1; p += rows_per_iter) {
-    const int64_t e0 = ((int64_t)b * S + p) * C + cv * kVec;
-    float v[kVec], d[kVec];
-    load8(x + e0, v);
-    load8(dy + e0, d);
+  auto row = [&](int64_t e0, float (&v)[kVec], const float (&d)[kVec]) {
 #pragma unroll
     for (int j = 0; j < kVec; ++j) {
       const float xh = (v[j] - mu[j]) * rs[j];
@@ -401,6 +453,28 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
       v[j] = rs[j] * (ga[j] * dz - c0[j] - xh * c1[j]);
     }
     store8(dx + e0, v);
+  };
+  int64_t p = p0 + r;
+  if constexpr (U > 1) {
+    for (; p + (U - 1) * rows_per_iter < p1; p += U * rows_per_iter) {
+      float v[U][kVec], d[U][kVec];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e0 = ((int64_t)b * S + p + u * rows_per_iter) * C + cv * kVec;
+        load8(x + e0, v[u]);
+        load8(dy + e0, d[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        row(((int64_t)b * S + p + u * rows_per_iter) * C + cv * kVec, v[u], d[u]);
+    }
+  }
+  for (; p < p1; p += rows_per_iter) {
+    const int64_t e0 = ((int64_t)b * S + p) * C + cv * kVec;
+    float v[kVec], d[kVec];
+    load8(x + e0, v);
+    load8(dy + e0, d);
+    row(e0, v, d);
   }
 }
 
@@ -447,20 +521,29 @@ int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, 
   float* part = reinterpret_cast<float*>(workspace);
   hipStream_t st = VD_STREAM(stream);
   const size_t lds = (size_t)p.rows_per_iter * C * sizeof(Stat);
+  const dim3 grid(p.nchunk, B);
+#define VD_GN_FWD(U)                                                                             \
+  gn_stats_kernel<T, U><<<grid, kThreads, lds, st>>>((const T*)x, S, C, G, p.chunk_px,          \
+                                                     p.rows_per_iter, part);                    \
+  gn_finalize_kernel<<<dim3(G, B), kThreads, 0, st>>>(part, p.nchunk, G, eps, mean, rstd);     \
+  if (silu)                                                                                      \
+    gn_apply_kernel<T, true, U><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean,      \
+                                                           rstd, (T*)y, S, C, G, p.chunk_px,    \
+                                                           p.rows_per_iter, drop);              \
+  else                                                                                           \
+    gn_apply_kernel<T, false, U><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean,     \
+                                                            rstd, (T*)y, S, C, G, p.chunk_px,   \
+                                                            p.rows_per_iter, drop)
   return VD_DISPATCH_DTYPE(dtype, T, {
-    gn_stats_kernel<T><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
-        (const T*)x, S, C, G, p.chunk_px, p.rows_per_iter, part);
-    gn_finalize_kernel<<<dim3(G, B), kThreads, 0, st>>>(part, p.nchunk, G, eps, mean, rstd);
-    const dim3 grid(p.nchunk, B);
-    if (silu)
-      gn_apply_kernel<T, true><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
-                                                          (T*)y, S, C, G, p.chunk_px,
-                                                          p.rows_per_iter, drop);
-    else
-      gn_apply_kernel<T, false><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean, rstd,
-                                                           (T*)y, S, C, G, p.chunk_px,
-                                                           p.rows_per_iter, drop);
+    if (kUnroll == 4) {
+      VD_GN_FWD(4);
+    } else if (kUnroll == 2) {
+      VD_GN_FWD(2);
+    } else {
+      VD_GN_FWD(1);
+    }
   });
+#undef VD_GN_FWD
 }
 
 int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, const float* beta,
@@ -480,29 +563,38 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
   hipStream_t st = VD_STREAM(stream);
   const size_t lds = (size_t)p.rows_per_iter * C * sizeof(float2);
   const dim3 grid(p.nchunk, B);
+  const int ksplit = (int)vd_cdiv(p.nchunk, kSumPer);
+#define VD_GN_BWD(U)                                                                             \
+  if (silu)                                                                                      \
+    gn_bwd_reduce_kernel<T, true, U><<<grid, kThreads, lds, st>>>(                               \
+        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,                 \
+        p.rows_per_iter, part, drop);                                                            \
+  else                                                                                           \
+    gn_bwd_reduce_kernel<T, false, U><<<grid, kThreads, lds, st>>>(                              \
+        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,                 \
+        p.rows_per_iter, part, drop);                                                            \
+  gn_bwd_sum_kernel<<<dim3((unsigned)vd_cdiv(C, 64), B, ksplit), 1024, 0, st>>>(                \
+      part, p.nchunk, C, kSumPer, sums);                                                         \
+  gn_bwd_finalize_kernel<<<1, kThreads, 0, st>>>(sums, ksplit, B, C, G, S, gamma, coef, dgamma,  \
+                                                 dbeta);                                          \
+  if (silu)                                                                                      \
+    gn_bwd_apply_kernel<T, true, U><<<grid, kThreads, 0, st>>>(                                  \
+        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,   \
+        p.rows_per_iter, drop);                                                                  \
+  else                                                                                           \
+    gn_bwd_apply_kernel<T, false, U><<<grid, kThreads, 0, st>>>(                                 \
+        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,   \
+        p.rows_per_iter, drop)
   return VD_DISPATCH_DTYPE(dtype, T, {
-    if (silu)
-      gn_bwd_reduce_kernel<T, true><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
-          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part, drop);
-    else
-      gn_bwd_reduce_kernel<T, false><<<dim3(p.nchunk, B), kThreads, lds, st>>>(
-          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, S, C, G, p.chunk_px,
-          p.rows_per_iter, part, drop);
-    const int ksplit = (int)vd_cdiv(p.nchunk, kSumPer);
-    gn_bwd_sum_kernel<<<dim3((unsigned)vd_cdiv(C, 64), B, ksplit), 1024, 0, st>>>(
-        part, p.nchunk, C, kSumPer, sums);
-    gn_bwd_finalize_kernel<<<1, kThreads, 0, st>>>(sums, ksplit, B, C, G, S, gamma, coef, dgamma,
-                                                   dbeta);
-    if (silu)
-      gn_bwd_apply_kernel<T, true><<<grid, kThreads, 0, st>>>(
-          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,
-          p.rows_per_iter, drop);
-    else
-      gn_bwd_apply_kernel<T, false><<<grid, kThreads, 0, st>>>(
-          (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,
-          p.rows_per_iter, drop);
+    if (kUnroll == 4) {
+      VD_GN_BWD(4);
+    } else if (kUnroll == 2) {
+      VD_GN_BWD(2);
+    } else {
+      VD_GN_BWD(1);
+    }
   });
+#undef VD_GN_BWD
 }
 
 }  // extern "C"
