@@ -394,7 +394,6 @@ def emit_check(st: Stream, V, u, masked, tag):
     """Lagged-max check of tile t-1 (its row sums in ps): any lane >= 2^16 (or inf / NaN) ->
     the rare path; then l += ps."""
     par = u & 1
-    tc = V.r("tc", 0)
     st.emit(f"v_cmp_ngt_f32 vcc, 0x47800000, {V.r('ps')}")
     st.raw(f"s_nop {CHECK_NOP}")
     st.raw(f"s_cbranch_vccz .Lfwd256_ok{tag}")
@@ -405,7 +404,6 @@ def emit_check(st: Stream, V, u, masked, tag):
     st.raw(f"s_swappc_b64 {S_RET}, s[{S_TGT + 2 * v}:{S_TGT + 2 * v + 1}]")
     st.label(f".Lfwd256_ok{tag}")
     st.emit(f"v_add_f32 {V.r('l')}, {V.r('l')}, {V.r('ps')}")
-    del tc
 
 
 def emit_body(st: Stream, V, A, u, masked_soft, tag, dma=True):
