@@ -233,18 +233,34 @@ class Stream:
         return "\n".join(self.lines) + "\n"
 
 
+# Code placement (MI355X_MICROARCH.md "Two waves per SIMD" item 8: a hand-written stream can
+# lose ~13 % under a uniform 4-byte shift): kernels named here start with one s_nop 0, which
+# shifts their whole instruction stream by 4 bytes.  VDIFF_ASM_PHASE (A/B builds,
+# tools/build_asm_phase.sh): "all", or a comma list of kernel names, flips the phase of those
+# kernels relative to this table.
+PHASE4 = set()
+
+
+def _phase4(name):
+    import os
+    env = os.environ.get("VDIFF_ASM_PHASE", "")
+    flip = env == "all" or name in env.split(",")
+    return (name in PHASE4) != flip
+
+
 def kernel_text(name, body, *, vgprs, agprs, sgprs, lds_bytes, kernarg_bytes, wg_size,
                 wg_ids=(1, 1, 1)):
     """(code + descriptor text, metadata entry) of one kernel (code object v5)."""
     accum = (vgprs + 3) // 4 * 4
     total = accum + agprs
     assert total <= 512, total
+    pad = "\ts_nop 0\n" if _phase4(name) else ""
     code = f""".text
 .globl {name}
 .p2align 8
 .type {name},@function
 {name}:
-{body}
+{pad}{body}
 \ts_endpgm
 .Lfunc_end_{name}:
 .size {name}, .Lfunc_end_{name}-{name}
