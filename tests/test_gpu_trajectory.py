@@ -18,7 +18,7 @@ import sys
 import pytest
 import torch
 
-from conftest import DROPIN, golden
+from conftest import DROPIN, golden, record_metric
 from oracle.fixtures import rel_l2, seeded
 from oracle.unet import audio_param_shapes, init_params
 
@@ -92,6 +92,8 @@ def _trajectory(case, bf16, tmp_path):
     unclamped = float((g[f"{case}_x0_10"].abs() < 1).float().mean())
     print("TRAJ", json.dumps({"case": case, "bf16": bf16, "unclamped_x0_frac": round(unclamped, 3),
                               **{k: float(f"{v:.3e}") for k, v in errs.items()}}))
+    record_metric(test="trajectory_vs_reference", case=case, mode="bf16" if bf16 else "fp32",
+                  unclamped_x0_frac=unclamped, **errs)
     return errs
 
 

@@ -1,14 +1,15 @@
 #!/bin/bash
-# Round-4 measurement set (GPU box), every step under its own time limit and chained:
+# End-of-round measurement set (GPU box), every step under its own time limit and chained:
 #   the whole -m gpu suite (no -x: every failure is listed), smoke(), the driver's bench
 #   command `python bench.py --steps 20 --warmup 5`, then rocprofv3 --kernel-trace --stats of
 #   that very command (its dQ + dK/dV averages reproduce roofline.frac), then the PMC passes
 #   of the attention kernels (HBM traffic per launch, D = 64 and D = 256).
-#   bash tools/final_r04.sh [tag] [skip-pmc]
+#   bash tools/final_round.sh [tag] [skip-pmc]
+#   The suite's measured parity errors go to gpurun_out/<tag>_parity_metrics.jsonl.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-T=${1:-r04}
-timeout -k 10 1000 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+T=${1:-r05}
+VDIFF_TEST_METRICS=gpurun_out/${T}_parity_metrics.jsonl timeout -k 10 1100 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/${T}_gpu_tests.log 2>&1
 rc=$?; grep -E "passed|failed" gpurun_out/${T}_gpu_tests.log | tail -2; grep FAILED gpurun_out/${T}_gpu_tests.log | head
 case $rc in 0|1) ;; *) echo "pytest rc=$rc: stopping"; exit $rc;; esac

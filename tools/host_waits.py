@@ -1,5 +1,5 @@
 """Where does the host wait in a train step?  Reads a rocprofv3 --hip-trace --kernel-trace
-database (tools/gpu_r04ab.sh) and prints, for the last complete step (steps cut at the
+database (a rocprofv3 --hip-runtime-trace run of bench.py) and prints, for the last complete step (steps cut at the
 q_sample kernels), the HIP API calls that took longest on the host (a synchronising call
 blocks until the GPU has drained) and the per-name totals of the calls that can block
 (…Synchronize, hipMemcpy without Async, hipMalloc / hipFree, hipHostMalloc …).
