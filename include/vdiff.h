@@ -67,6 +67,20 @@ int vd_q_sample(const void* x0, const void* eps, void* xt, const int64_t* t,
                 const float* sqrt_acp, const float* sqrt_1m_acp,
                 int64_t B, int64_t per_sample, int dtype, void* stream);
 
+/* ---- MSE loss (train.py:103 nn.MSELoss(), :130 loss = criterion(noise_pred, noise)) ----
+ * out[0] = mean((pred - target)^2) over n elements of `dtype`, fp32, in a FIXED order:
+ * per-block partial sums of fixed ranges into the caller's workspace
+ * (vd_mse_loss_workspace_size(n) bytes), then one block sums them in block order.  Two
+ * launches, no semaphore and no memset, so the value is identical eager and replayed from
+ * a HIP graph.  pred / target 16-B aligned.
+ * vd_mse_loss_bwd: grad_pred = 2 (pred - target) / n * grad_loss[0] (grad_loss: device fp32
+ * scalar, the autograd seed; MSELoss.backward). */
+size_t vd_mse_loss_workspace_size(int64_t n);
+int vd_mse_loss(const void* pred, const void* target, int64_t n, int dtype, float* out,
+                void* workspace, size_t workspace_bytes, void* stream);
+int vd_mse_loss_bwd(const void* pred, const void* target, const float* grad_loss, int64_t n,
+                    int dtype, void* grad_pred, void* stream);
+
 /* p_sample V1: linear_noise_scheduler.py:48-76 (LinearNoiseScheduler.
  * sample_prev_timestep).  x0 = clamp((xt - s1m[t] eps) / sqrt(acp[t])),
  * mean = (xt - beta[t] eps / s1m[t]) / sqrt(alpha[t]); t == 0 returns mean,

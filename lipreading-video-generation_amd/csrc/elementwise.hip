@@ -249,6 +249,95 @@ __global__ void upsample_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx
   }
 }
 
+// ------------------------------------------------------------ MSE loss (train.py:103, 130)
+// Fixed-order two-launch reduction: mse_partial_kernel sums a fixed contiguous range per
+// block (8 elements per lane, a lane's sum, then an LDS tree) into partial[block];
+// mse_finish_kernel (one block) sums the partials in block order and scales by 1/n.  No
+// semaphore, no memset, no cross-block communication inside a launch: the same bits every
+// run, eager or replayed from a HIP graph (torch's one-launch multi-block
+// mean -- a hipMemsetAsync'd semaphore plus a last-block combine -- returned stale values
+// when replayed under HIP's graph packet capture).
+constexpr int kMseBlocks = 1024;
+
+inline int mse_blocks(int64_t n) {
+  const int64_t per = (int64_t)kBlock * 8;
+  const int64_t g = vd_cdiv(n, per);
+  return (int)(g < kMseBlocks ? (g > 0 ? g : 1) : kMseBlocks);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) mse_partial_kernel(
+    const T* __restrict__ pred, const T* __restrict__ tgt, int64_t n, int64_t chunk,
+    float* __restrict__ partial) {
+  __shared__ float red[kBlock];
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  float s = 0.f;
+  // chunk is a multiple of 8: every 8-vector lies in one block's range
+  for (int64_t i = lo + (int64_t)threadIdx.x * 8; i < hi; i += (int64_t)kBlock * 8) {
+    if (i + 8 <= hi) {
+      float a[8], b[8];
+      load8(pred + i, a);
+      load8(tgt + i, b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = a[k] - b[k];
+        s = fmaf(d, d, s);
+      }
+    } else {
+      for (int64_t j = i; j < hi; ++j) {
+        const float d = Elem<T>::ld(pred + j) - Elem<T>::ld(tgt + j);
+        s = fmaf(d, d, s);
+      }
+    }
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(kBlock) mse_finish_kernel(const float* __restrict__ partial,
+                                                            int nblocks, float inv_n,
+                                                            float* __restrict__ out) {
+  __shared__ float red[kBlock];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nblocks; i += kBlock) s += partial[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0] * inv_n;
+}
+
+// d loss / d pred = 2 (pred - tgt) / n * g, g = the loss gradient (a device scalar)
+template <typename T>
+__global__ void __launch_bounds__(kBlock) mse_bwd_kernel(
+    const T* __restrict__ pred, const T* __restrict__ tgt, const float* __restrict__ gout,
+    float scale, int64_t n, T* __restrict__ gpred) {
+  const float c = scale * *gout;
+  const int64_t nv = n / 8;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    float a[8], b[8];
+    load8(pred + 8 * v, a);
+    load8(tgt + 8 * v, b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = c * (a[k] - b[k]);
+    store8(gpred + 8 * v, a);
+  }
+  for (int64_t j = nv * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x)
+    Elem<T>::st(gpred + j, c * (Elem<T>::ld(pred + j) - Elem<T>::ld(tgt + j)));
+}
+
 }  // namespace
 
 
@@ -403,6 +492,55 @@ __global__ void pack_weights_kernel(const vd_pack_desc* __restrict__ descs, int 
 }
 
 extern "C" {
+
+size_t vd_mse_loss_workspace_size(int64_t n) {
+  return (size_t)mse_blocks(n) * sizeof(float);
+}
+
+int vd_mse_loss(const void* pred, const void* target, int64_t n, int dtype, float* out,
+                void* workspace, size_t workspace_bytes, void* stream) {
+  VD_REQUIRE(pred && target && out && workspace, "null argument");
+  VD_REQUIRE(n > 0, "empty tensor");
+  VD_REQUIRE(dtype == VD_F32 || dtype == VD_BF16, "bad dtype %d", dtype);
+  VD_REQUIRE((reinterpret_cast<uintptr_t>(pred) | reinterpret_cast<uintptr_t>(target)) % 16 == 0,
+             "pred / target must be 16-B aligned");
+  const int nb = mse_blocks(n);
+  VD_REQUIRE(workspace_bytes >= (size_t)nb * sizeof(float), "workspace too small");
+  const int64_t chunk = vd_cdiv(vd_cdiv(n, nb), 8) * 8;
+  float* partial = static_cast<float*>(workspace);
+  hipStream_t st = VD_STREAM(stream);
+  if (dtype == VD_F32)
+    mse_partial_kernel<float><<<nb, kBlock, 0, st>>>(static_cast<const float*>(pred),
+                                                     static_cast<const float*>(target), n,
+                                                     chunk, partial);
+  else
+    mse_partial_kernel<bf16_t><<<nb, kBlock, 0, st>>>(static_cast<const bf16_t*>(pred),
+                                                      static_cast<const bf16_t*>(target), n,
+                                                      chunk, partial);
+  mse_finish_kernel<<<1, kBlock, 0, st>>>(partial, nb, (float)(1.0 / (double)n), out);
+  return vd::check_launch("vd_mse_loss");
+}
+
+int vd_mse_loss_bwd(const void* pred, const void* target, const float* grad_loss, int64_t n,
+                    int dtype, void* grad_pred, void* stream) {
+  VD_REQUIRE(pred && target && grad_loss && grad_pred, "null argument");
+  VD_REQUIRE(n > 0, "empty tensor");
+  VD_REQUIRE(dtype == VD_F32 || dtype == VD_BF16, "bad dtype %d", dtype);
+  VD_REQUIRE((reinterpret_cast<uintptr_t>(pred) | reinterpret_cast<uintptr_t>(target) |
+              reinterpret_cast<uintptr_t>(grad_pred)) % 16 == 0, "buffers must be 16-B aligned");
+  const float scale = (float)(2.0 / (double)n);
+  hipStream_t st = VD_STREAM(stream);
+  const int g = grid_for(vd_cdiv(n, 8));
+  if (dtype == VD_F32)
+    mse_bwd_kernel<float><<<g, kBlock, 0, st>>>(static_cast<const float*>(pred),
+                                                static_cast<const float*>(target), grad_loss,
+                                                scale, n, static_cast<float*>(grad_pred));
+  else
+    mse_bwd_kernel<bf16_t><<<g, kBlock, 0, st>>>(static_cast<const bf16_t*>(pred),
+                                                 static_cast<const bf16_t*>(target), grad_loss,
+                                                 scale, n, static_cast<bf16_t*>(grad_pred));
+  return vd::check_launch("vd_mse_loss_bwd");
+}
 
 int vd_timestep_embedding(const int64_t* t, int B, int dim, float max_period, float* out,
                           void* stream) {

@@ -109,6 +109,9 @@ _SIGS = {
     "vd_layernorm_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _sz,
                               _vp]),
     "vd_gelu_tanh": (_i, [_vp, _vp, _i64, _i, _vp]),
+    "vd_mse_loss_workspace_size": (_sz, [_i64]),
+    "vd_mse_loss": (_i, [_vp, _vp, _i64, _i, _vp, _vp, _sz, _vp]),
+    "vd_mse_loss_bwd": (_i, [_vp, _vp, _vp, _i64, _i, _vp, _vp]),
     "vd_gelu_tanh_bwd": (_i, [_vp, _vp, _vp, _i64, _i, _vp]),
 }
 

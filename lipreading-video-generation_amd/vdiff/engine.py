@@ -17,7 +17,6 @@ import warnings
 from dataclasses import dataclass
 
 import torch
-import torch.nn.functional as F
 
 from . import ops
 from .ddp import GradBucketer
@@ -70,15 +69,18 @@ class Trainer:
     train.py:102-103: Adam(model.parameters(), lr=1e-2), MSELoss."""
 
     def __init__(self, model, scheduler, lr=1e-2, bucket_mb=25.0, fused_adam=True,
-                 check_every=50, batch_pack=True, graph=False):
+                 check_every=50, batch_pack=True, graph=False, loss_fn=None):
         """check_every: the loss finiteness flag (kept on the device, updated every step) is
         read on the host every `check_every` steps and by check_finite(); a non-finite
         loss raises FloatingPointError naming the first bad step.  0 disables it.
         batch_pack: re-pack the conv operands once per step in one launch
         (ops.step_packed_weights) instead of per conv call.
         graph: replay the denoiser's forward + backward as one HIP graph (TrainStepGraph);
-        one process only."""
+        one process only.
+        loss_fn: (pred, eps) -> scalar loss; default ops.mse_loss (vd_mse_loss, fixed-order).
+        Host-logic tests on CPU pass torch's F.mse_loss (the product ops refuse CPU tensors)."""
         self.model = model
+        self.loss_fn = loss_fn or ops.mse_loss
         self.scheduler = scheduler
         self.check_every = int(check_every)
         self.steps_done = 0
@@ -100,9 +102,9 @@ class Trainer:
                              "frozen into the graph)")
         if graph and os.environ.get("VDIFF_TRAIN_GRAPH_EXPERIMENTAL") != "1":
             # advisor r03: a known defect must not be one keyword away from a user
-            raise RuntimeError("Trainer(graph=True) is experimental: at the config-2 scale its "
-                               "replays returned negative / non-finite losses (DESIGN section 9 "
-                               "item 3); set VDIFF_TRAIN_GRAPH_EXPERIMENTAL=1 to run it anyway")
+            raise RuntimeError("Trainer(graph=True) is opt-in: it measured no gain over the eager "
+                               "step (kernel-bound; DESIGN section 9 item 3); set "
+                               "VDIFF_TRAIN_GRAPH_EXPERIMENTAL=1 to run it")
         self.graph = TrainStepGraph(self) if graph else None
 
     def step(self, clip: Clip) -> torch.Tensor:
@@ -115,7 +117,7 @@ class Trainer:
         with self.packs:
             xt = self.scheduler.add_noise(clip.x0, clip.eps, clip.t)
             pred = self.model(xt, clip.cond, clip.audio, clip.t)
-            loss = F.mse_loss(pred, clip.eps)
+            loss = self.loss_fn(pred, clip.eps)
             loss.backward()
         if self.bucketer is not None:
             self.bucketer.finish()
@@ -175,9 +177,8 @@ class TrainStepGraph:
     ~600 launch gaps of an eager step).
 
     Captured: the batched weight pack, q_sample, the conditioning concat and the UNet forward,
-    the MSE and the whole backward down to the UNet parameters' gradients and the gradient of
-    the pooled audio features; the reported loss is the eager MSE of the replayed prediction
-    (_body).  Eager around it: the wav2vec2 encoder (transformers draws its
+    the MSE (vd_mse_loss, whose value step() returns) and the whole backward down to the UNet
+    parameters' gradients and the gradient of the pooled audio features.  Eager around it: the wav2vec2 encoder (transformers draws its
     LayerDrop and SpecAugment decisions on the host every step, which changes the launch
     sequence, so it cannot be frozen), its backward (fed the replayed feature gradient) and
     the fused Adam step over all parameters.  Same math as the eager step: the first `warmup`
@@ -222,32 +223,35 @@ class TrainStepGraph:
         for p in self.eager_params:
             p.grad = None
         self.steps += 1
-        # the loss is computed here, eagerly, from the replay's own prediction: the MSE the
-        # graph captured is only the backward's seed (see _body)
-        with torch.no_grad():
-            loss = F.mse_loss(self.pred, self.eps)
+        loss = self.loss.clone()  # the replay's own MSE (vd_mse_loss, captured)
         tr._track_finite(loss)
         return loss
+
+    def node_types(self):
+        """{node type: count} of the captured graph (vdiff.hipgraph; memset nodes must be 0)."""
+        from .hipgraph import graph_nodes
+        nodes = graph_nodes(self.g.raw_cuda_graph())
+        return {t: sum(1 for n in nodes if n["type"] == t) for t in {n["type"] for n in nodes}}
 
     @staticmethod
     def _shapes(clip, enc):
         return tuple((tuple(x.shape), x.dtype) for x in (clip.x0, clip.eps, clip.t, clip.cond, enc))
 
     def _body(self):
-        """The captured region.  Its MSE seeds the backward only (d mean((p - e)^2) / dp does
-        not read the forward's value): the forward VALUE of torch's multi-block mean, replayed
-        in this graph, came out wrong from the third replay on in runs whose host code did
-        other GPU reductions between replays (round 4: -0.855 for 9.03 at 64x64x16, while every
-        gradient and every weight stayed bit-identical to the eager step; the value was already
-        wrong when copied out right after the MSE, inside the graph; tools/graph_loss_probe.py,
-        profiles/r04j_graph_loss_probe.txt).  step() therefore reports the MSE of the kept
-        prediction buffer, computed eagerly -- the eager step's own op on the same values."""
+        """The captured region.  The loss is vd_mse_loss (ops.mse_loss), a fixed-order
+        two-launch reduction: round 4 found torch's one-launch multi-block mean (per-block
+        partials, a semaphore reset by a captured hipMemsetAsync, a last-block combine)
+        returning a stale value from some replay on -- the replay's output kept an earlier
+        value while every gradient stayed exact -- and round 5 reproduced that with torch alone
+        (tools/graph_reduce_repro.py) and saw it vanish under DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+        (DESIGN section 9.3).  The captured step holds no memset node
+        (tests/test_gpu_train_graph.py), and step() returns this in-graph value."""
         tr = self.tr
         with tr.packs:
             xt = tr.scheduler.add_noise(self.x0, self.eps, self.t)
             pred = tr.model(xt, self.cond, self.feats, self.t)
-            self.pred = pred.detach()  # lives in the graph's pool, rewritten by each replay
-            loss = F.mse_loss(pred, self.eps)
+            loss = tr.loss_fn(pred, self.eps)
+            self.loss = loss.detach()  # lives in the graph's pool, rewritten by each replay
             loss.backward()
 
     def _capture(self, clip, enc):
@@ -270,7 +274,7 @@ class TrainStepGraph:
         torch.cuda.current_stream().wait_stream(side)
         tr.opt.zero_grad(set_to_none=True)
         self.feats.grad = None
-        self.g = torch.cuda.CUDAGraph()
+        self.g = torch.cuda.CUDAGraph(keep_graph=True)  # node list kept (graph_nodes)
         lib = _lib.lib()
         lib.vd_set_dropout_counter(self.ctr.data_ptr())
         try:
@@ -279,6 +283,7 @@ class TrainStepGraph:
                 self._body()
         finally:
             lib.vd_set_dropout_counter(None)
+        self.g.instantiate()
         self.shapes = self._shapes(clip, enc)
         tr.packs.frozen = True  # the graph replays the pack launch into these buffers
         self.grads = [(p, p.grad) for p in model.parameters() if p.grad is not None]

@@ -1,7 +1,7 @@
 """Nodes of a captured HIP graph through the HIP runtime's own C API (ctypes on
-libamdhip64.so): node types, and for memset nodes the destination, size and value.  Used by
-the graph-replay tests (no memset node may sit in a captured train step)
-and by tools/graph_reduce_repro.py.  torch: capture with torch.cuda.CUDAGraph(keep_graph=True)
+libamdhip64.so): node types, and for memset nodes the destination, size and value.  A
+diagnostic: TrainStepGraph.node_types(), the graph-replay tests (no memset node may sit in a
+captured train step) and tools/graph_reduce_repro.py.  torch: capture with torch.cuda.CUDAGraph(keep_graph=True)
 and pass graph.raw_cuda_graph()."""
 import ctypes
 

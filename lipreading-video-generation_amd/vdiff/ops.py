@@ -266,6 +266,42 @@ def silu(x):
     return SiLUFn.apply(x)
 
 
+class MSELossFn(torch.autograd.Function):
+    """mean((pred - target)^2) (train.py:103, 130: nn.MSELoss()(noise_pred, noise)) on
+    vd_mse_loss: a fixed-order two-launch reduction, so the loss has the same bits eager and
+    replayed from a HIP graph; the gradient is vd_mse_loss_bwd."""
+
+    @staticmethod
+    def forward(ctx, pred, target):
+        _gpu(pred, target)
+        if pred.shape != target.shape:
+            raise ValueError(f"mse_loss: shapes {tuple(pred.shape)} / {tuple(target.shape)}")
+        dt = torch.promote_types(pred.dtype, target.dtype)
+        p, t = pred.to(dt).contiguous(), target.to(dt).contiguous()
+        n = p.numel()
+        out = torch.empty((), dtype=torch.float32, device=p.device)
+        nws = _lib.lib().vd_mse_loss_workspace_size(n)
+        ws = torch.empty(nws, dtype=torch.uint8, device=p.device)
+        _lib.call("vd_mse_loss", _p(p), _p(t), n, _dtype(p), _p(out), _p(ws), nws, _stream(p))
+        ctx.save_for_backward(p, t)
+        ctx.pred_dtype = pred.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p, t = ctx.saved_tensors
+        g = g.detach().float().contiguous()
+        dp = torch.empty_like(p)
+        _lib.call("vd_mse_loss_bwd", _p(p), _p(t), _p(g), p.numel(), _dtype(p), _p(dp),
+                  _stream(p))
+        return dp.to(ctx.pred_dtype), None
+
+
+def mse_loss(pred, target):
+    """The denoiser's training loss (fp32 scalar); the target gets no gradient."""
+    return MSELossFn.apply(pred, target)
+
+
 def linear(x, weight, bias=None, residual=None):
     """x [..., Cin] @ weight[Cout, Cin]^T + bias (+ residual [..., Cout], fused into the
     epilogue) on the implicit-GEMM kernel (1x1 conv)."""

@@ -277,6 +277,14 @@ class VivitTrainer:
             self.graph_opt.replay()
         return self.static_loss
 
+    def node_types(self):
+        """{node type: count} of the captured step graph (vdiff.hipgraph): the graph must hold
+        no memset node -- torch's reductions that reset a semaphore by a captured memset went
+        stale under HIP's graph packet capture."""
+        from .hipgraph import graph_nodes
+        nodes = graph_nodes(self.graph.raw_cuda_graph())
+        return {t: sum(1 for n in nodes if n["type"] == t) for t in {n["type"] for n in nodes}}
+
     def _fwd_bwd(self, x, y):
         self.model.train()
         loss = F.cross_entropy(self.model(x), y)
@@ -306,10 +314,11 @@ class VivitTrainer:
                     self._step(self.static_x, self.static_y)
         torch.cuda.current_stream(dev).wait_stream(side)
         self.opt.zero_grad(set_to_none=True)
-        self.graph = torch.cuda.CUDAGraph()
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)  # node list kept (node_types)
         if not self.distributed:
             with torch.cuda.graph(self.graph):
                 self.static_loss = self._step(self.static_x, self.static_y, zero=False)
+            self.graph.instantiate()
             self._restore(snapshot)
             return
         # parameters with a gradient (the pooler has none: the classifier never reads it).

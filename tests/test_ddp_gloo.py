@@ -50,7 +50,9 @@ def _worker(rank, world, port, out):
         if step == 0:
             bk.zero_grad()
     if rank == 0:
-        out.put([p.grad.clone() for p in m.parameters()] + [torch.tensor(len(bk.buckets))])
+        # numpy arrays travel by value: a tensor would travel as a shared-memory fd whose
+        # sharer thread dies with this process, racing the parent's get()
+        out.put([p.grad.detach().numpy().copy() for p in m.parameters()] + [len(bk.buckets)])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -64,6 +66,7 @@ def test_bucketed_allreduce_matches_single_process():
     for p in procs:
         p.start()
     got = q.get(timeout=240)
+    got = [torch.from_numpy(a) for a in got[:-1]] + [torch.tensor(got[-1])]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -117,7 +120,9 @@ def _skip_worker(rank, world, port, out):
         if step == 0:
             bk.zero_grad()
     if rank == 0:
-        out.put([p.grad.clone() for p in m.parameters()] + [torch.tensor(len(bk.buckets))])
+        # numpy arrays travel by value: a tensor would travel as a shared-memory fd whose
+        # sharer thread dies with this process, racing the parent's get()
+        out.put([p.grad.detach().numpy().copy() for p in m.parameters()] + [len(bk.buckets)])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -133,6 +138,7 @@ def test_bucket_order_survives_rank_dependent_unused_params():
     for p in procs:
         p.start()
     got = q.get(timeout=240)
+    got = [torch.from_numpy(a) for a in got[:-1]] + [torch.tensor(got[-1])]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

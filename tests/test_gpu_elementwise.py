@@ -219,3 +219,44 @@ def test_cond_concat_bwd_matches_torch(dtype, hw):
     tol = 1e-6 if dtype == torch.float32 else 1e-2
     assert rel_l2(outs[0][0], ir.grad) < tol, rel_l2(outs[0][0], ir.grad)
     assert rel_l2(outs[0][1], ar.grad) < tol, rel_l2(outs[0][1], ar.grad)
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 196608, 786432, 3 * 25 * 256 * 256 + 5])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mse_loss(n, dtype):
+    """vd_mse_loss / vd_mse_loss_bwd (train.py:103, 130) against torch's MSELoss in float64
+    on the same values: the fp32 fixed-order sum within 1e-6 relative (bf16 inputs are
+    exact in fp32), the same bits on a second run, and the gradient 2 (p - e) / n * g."""
+    from vdiff import ops
+    g = torch.Generator(device=dev).manual_seed(n)
+    p = torch.randn(n, generator=g, device=dev).to(dtype).requires_grad_(True)
+    e = torch.randn(n, generator=g, device=dev).to(dtype)
+    loss = ops.mse_loss(p, e)
+    ref = torch.nn.functional.mse_loss(p.double(), e.double())
+    assert loss.dtype == torch.float32 and loss.shape == ()
+    assert abs(float(loss) - float(ref)) <= 1e-6 * float(ref), (float(loss), float(ref))
+    assert torch.equal(ops.mse_loss(p, e), loss)
+    gs = torch.tensor(0.37, device=dev)
+    gp, = torch.autograd.grad(loss, p, gs)
+    gr = (2.0 / n) * (p.detach().float() - e.float()) * 0.37
+    assert gp.dtype == dtype
+    assert rel_l2(gp.float(), gr) < (1e-6 if dtype == torch.float32 else 4e-3)
+
+
+def test_mse_loss_mixed_dtype_and_layout():
+    """bf16 prediction against an fp32 target promotes to fp32 (F.mse_loss's rule; the
+    gradient comes back in bf16), and a channels-last prediction is compared element by
+    element in logical order."""
+    from vdiff import ops
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn((1, 3, 4, 16, 16), generator=g, device=dev)
+    e = torch.randn(x.shape, generator=g, device=dev)
+    pb = x.bfloat16().requires_grad_(True)
+    loss = ops.mse_loss(pb, e)
+    ref = torch.nn.functional.mse_loss(pb.detach().double(), e.double())
+    assert abs(float(loss) - float(ref)) <= 1e-6 * float(ref)
+    gp, = torch.autograd.grad(loss, pb)
+    assert gp.dtype == torch.bfloat16
+    pc = ops.to_cl(x)
+    assert abs(float(ops.mse_loss(pc, e)) - float(torch.nn.functional.mse_loss(x, e))) <= \
+        1e-6 * float(torch.nn.functional.mse_loss(x, e))

@@ -268,12 +268,15 @@ def test_graph_config2_lr0_replays_equal_eager():
 
 
 def test_graph_loss_with_moving_weights_and_host_reductions():
-    """The round-4 reproducer of the negative replay losses: 64x64x16, lr 1e-2 (the weights
-    move), an eager twin stepped alternately, and torch.equal over every parameter pair after
-    each step (host-side GPU reductions between the replays).  Before the fix the replayed
-    step returned -0.855 and -0.707 (bf16-exact garbage) at steps 4-5 while every weight and
-    gradient stayed bit-identical; the loss now comes from the replay's prediction and must
-    equal the twin's exactly at every step."""
+    """The round-4 reproducer of the wrong replay losses: 64x64x16, lr 1e-2 (the weights
+    move), an eager twin stepped alternately, and torch.equal over every parameter pair plus
+    clones and sums of every gradient after each step (host-side GPU work between the
+    replays).  Round 4 saw -0.855 and -0.707 (bf16-exact garbage) at steps 4-5 from torch's
+    in-graph mean while every weight and gradient stayed bit-identical; round 5 traced it to
+    that reduction under HIP's graph packet capture and replaced it with
+    vd_mse_loss.  The value returned is the graph's OWN captured loss, and it must equal the
+    eager twin's bit for bit at every one of 12 steps; the captured graph holds no memset
+    node."""
     from vdiff.engine import Trainer
     from vdiff.schedulers import LinearNoiseScheduler
     m = _bench_unet(64, 0.0)
@@ -282,11 +285,34 @@ def test_graph_loss_with_moving_weights_and_host_reductions():
     tg = Trainer(m, sched, lr=1e-2, graph=True)
     te = Trainer(twin, sched, lr=1e-2)
     clip = _bench_clip(64)
-    for step in range(8):
+    for step in range(12):
         le = float(te.step(clip))
         lg = float(tg.step(clip))
         assert lg >= 0.0 and lg == le, (step, le, lg)
         assert all(torch.equal(a, b) for a, b in zip(twin.parameters(), m.parameters())), step
+        kept = [p.grad.clone() for p in m.parameters() if p.grad is not None]
+        assert all(torch.isfinite(k.abs().sum()) for k in kept)
+    types = tg.graph.node_types()
+    assert types.get("memset", 0) == 0 and types.get("kernel", 0) > 100, types
+
+
+def test_graph_step_holds_no_memset_nodes():
+    """The captured train step (tiny model, trainable wav2vec2 fed by the replayed feature
+    gradient) contains no memset node, whose replay under HIP's graph
+    packet capture is where torch's in-graph reduction went stale -- and
+    its in-graph loss equals the eager step's over five replays at lr 0."""
+    from vdiff.engine import Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    m = _model(audio=True)
+    me = copy.deepcopy(m)
+    sched = LinearNoiseScheduler(100, 0.00085, 0.012)
+    tg = Trainer(m, sched, lr=0.0, graph=True)
+    te = Trainer(me, sched, lr=0.0)
+    c = _clip(0, True)
+    for _ in range(7):
+        assert torch.equal(tg.step(c), te.step(c))
+    types = tg.graph.node_types()
+    assert types.get("memset", 0) == 0 and types["kernel"] > 20, types
 
 
 def test_graph_config2_dropout_replays():

@@ -3,6 +3,7 @@ loss finiteness record is kept on the device and read only every check_every ste
 check_finite(), and it names the first bad step (SURVEY 5 failure detection)."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 from vdiff.engine import Clip, Trainer
 
@@ -31,7 +32,7 @@ def _clip():
 
 
 def test_nonfinite_loss_raises_with_first_step():
-    tr = Trainer(_Model({3, 5}), _Sched(), lr=1e-3, check_every=4)
+    tr = Trainer(_Model({3, 5}), _Sched(), lr=1e-3, loss_fn=F.mse_loss, check_every=4)
     c = _clip()
     for _ in range(3):
         tr.step(c)
@@ -40,14 +41,14 @@ def test_nonfinite_loss_raises_with_first_step():
 
 
 def test_check_finite_between_reads_and_disabled():
-    tr = Trainer(_Model({1}), _Sched(), lr=1e-3, check_every=100)
+    tr = Trainer(_Model({1}), _Sched(), lr=1e-3, loss_fn=F.mse_loss, check_every=100)
     c = _clip()
     tr.step(c)
     tr.check_finite()  # finite so far
     tr.step(c)         # NaN at step 1: not read yet (no host sync per step)
     with pytest.raises(FloatingPointError, match="step 1 "):
         tr.check_finite()
-    off = Trainer(_Model({0}), _Sched(), lr=1e-3, check_every=0)
+    off = Trainer(_Model({0}), _Sched(), lr=1e-3, loss_fn=F.mse_loss, check_every=0)
     off.step(c)
     off.check_finite()
 
@@ -61,7 +62,7 @@ def _ddp_worker(rank, world, port, q):
     torch.manual_seed(0)
     m = _Model({2} if rank == 1 else set())  # rank 1 alone goes non-finite at step 2
     broadcast_parameters(m)
-    tr = Trainer(m, _Sched(), lr=1e-3, check_every=4)
+    tr = Trainer(m, _Sched(), lr=1e-3, loss_fn=F.mse_loss, check_every=4)
     c = _clip()
     res = "no raise"
     try:
@@ -96,8 +97,8 @@ def test_ddp_nonfinite_loss_raises_on_every_rank():
 
 
 def test_graph_trainer_is_gated(monkeypatch):
-    """Advisor r03: Trainer(graph=True) (replays with a known defect at the config-2 scale)
-    raises unless VDIFF_TRAIN_GRAPH_EXPERIMENTAL=1 opts in."""
+    """Advisor r03: Trainer(graph=True) stays opt-in (it measured no gain over the eager step,
+    DESIGN section 9 item 3): it raises unless VDIFF_TRAIN_GRAPH_EXPERIMENTAL=1."""
     monkeypatch.delenv("VDIFF_TRAIN_GRAPH_EXPERIMENTAL", raising=False)
     with pytest.raises(RuntimeError, match="VDIFF_TRAIN_GRAPH_EXPERIMENTAL"):
         Trainer(_Model(set()), _Sched(), lr=1e-3, graph=True)

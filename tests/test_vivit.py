@@ -10,7 +10,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import golden
+from conftest import record_metric, golden
 from oracle.fixtures import rel_l2, seeded
 from oracle.vivit import gelu_fast, seeded_state, vivit_classifier, vivit_forward
 
@@ -173,8 +173,13 @@ def test_gelu_tanh_kernel(dtype):
 
 @pytest.mark.gpu
 def test_vivit_graph_step_matches_eager():
-    """The HIP-graph-captured step (forward + backward + AdamW replayed) follows the same
-    trajectory as the eager step from the same weights (fp32)."""
+    """the HIP-graph step (forward + backward + AdamW replayed; the path
+    the bench's config-5 leg times at N = 1) against the eager step from the same weights
+    (fp32), step by step: the graph's OWN captured loss (static_loss, read after each replay)
+    equals the eager loss to 1e-6 at every one of six steps, and every parameter after the
+    last step agrees to 1e-6 rel-L2.  The capture's three warm-up updates are undone by
+    _restore (weights and AdamW moments), so the first replay is the first update.  The
+    captured graph holds no memset node."""
     from vdiff.vivit import VivitTrainer
     xs = [seeded((16, 5, 1, 32, 32), 20 + i).to(dev) for i in range(6)]
     ys = [torch.randint(0, CLASSES, (16,), generator=torch.Generator().manual_seed(i)).to(dev)
@@ -185,13 +190,19 @@ def test_vivit_graph_step_matches_eager():
         m.load_state_dict(_state(m))
         m = m.to(dev)
         tr = VivitTrainer(m, graph=graph)
-        losses = [float(tr.step(x, y)) for x, y in zip(xs, ys)]
-        runs.append((losses, m.vit.layers[0].mlp.fc1.weight.detach().clone()))
-    (le, we), (lg, wg) = runs
-    assert all(v == v for v in lg)
-    # the graph trainer took 3 extra warm-up steps on batch 0 before its first replay
-    assert lg[-1] < le[0] * 1.5
-    assert rel_l2(wg, we) < 5e-2
+        losses = []
+        for x, y in zip(xs, ys):
+            losses.append(float(tr.step(x, y)))   # graph: static_loss after the replay
+        runs.append((losses, [p.detach().clone() for p in m.parameters()], tr))
+    (le, we, _), (lg, wg, tg) = runs
+    record_metric(test="vivit_graph_vs_eager", losses_eager=le, losses_graph=lg,
+                  max_weight_rel_l2=max(rel_l2(a, b) for a, b in zip(wg, we)))
+    for i, (a, b) in enumerate(zip(lg, le)):
+        assert abs(a - b) <= 1e-6 * abs(b), (i, lg, le)
+    for a, b in zip(wg, we):
+        assert rel_l2(a, b) <= 1e-6
+    types = tg.node_types()
+    assert types.get("memset", 0) == 0 and types.get("kernel", 0) > 50, types
 
 
 @pytest.mark.gpu

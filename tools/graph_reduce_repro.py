@@ -78,8 +78,9 @@ def main():
     grads = [p.grad for p in params]
     sems, sem_log = [], []
     if a.probe_sem:
-        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-        from hipgraph import graph_nodes, read_i32
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+            __file__))), "lipreading-video-generation_amd"))
+        from vdiff.hipgraph import graph_nodes, read_i32
         nodes = graph_nodes(g.raw_cuda_graph())
         sems = [nd for nd in nodes if nd["type"] == "memset"]
         print(json.dumps({"node_types": {t: sum(1 for nd in nodes if nd["type"] == t)
