@@ -13,7 +13,8 @@ train.py:88-97 with dims=3 (model_channels 64, mult (1,2,4), 2 res blocks,
 attention at every level, 1 head, 195 input channels), joint attention over all
 T*H*W tokens (the reference semantics), bf16 activations / fp32 master weights,
 dropout 0.1 in train mode, random-init wav2vec2-base audio encoder (trainable, as
-the reference), Adam lr 1e-2.  One synthetic clip [1, 3, 16, 128, 128] (+16 audio
+the reference), Adam at --lr (default 1e-3; train.py:102 uses 1e-2, at which this init
+diverges within 25 steps -- DESIGN section 5).  One synthetic clip [1, 3, 16, 128, 128] (+16 audio
 windows of 4000 samples) per GPU, resident in HBM before timing.  A step = q_sample
 + forward + MSE + backward + RCCL gradient all-reduce + Adam.  Weak scaling.
 
@@ -86,6 +87,10 @@ def parse():
                          "at --lr like the headline; -1 (default): --steps, so both legs time "
                          "the same step indices (the clock follows the weights, DESIGN 5); "
                          "0 skips it")
+    ap.add_argument("--st-steps", type=int, default=-1,
+                    help="timed train steps of the spatial_temporal leg (auxiliary: the build's "
+                         "default attention mode, SURVEY D1) after --warmup untimed ones; -1: "
+                         "--steps; 0 skips it")
     ap.add_argument("--train-graph", action="store_true",
                     help="auxiliary leg: graph-replayed train step paired with an eager one "
                          "(DESIGN section 9 item 3)")
@@ -424,6 +429,95 @@ def xattn_leg(args, rank, world, device, base_ms):
     return out
 
 
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 6.29 TB/s measured copy)
+
+
+def short_attention_roofline(summary):
+    """Per-kernel rows of the short-sequence (temporal, <= 32 tokens) attention launches in a
+    timer summary: HBM-bound, so achieved = algorithmic bytes per launch
+    (vdiff.flops.short_attention_bytes) / average launch time, against the HBM peak; plus the
+    executed / algorithmic FLOP ratio (tile padding x recomputed products)."""
+    from vdiff.flops import attention_kernel_flops, short_attention_bytes
+    rows = []
+    for (kind, hd, n, nseq), (cnt, tot_ms) in summary.items():
+        if n > 32 or kind not in ("attn_fwd", "attn_bwd"):
+            continue
+        avg_s = tot_ms / cnt / 1e3
+        nb = short_attention_bytes(kind, n, hd, nseq)
+        lp = 16 if n <= 16 else 32
+        ex = attention_kernel_flops(kind, lp, hd, nseq) * (5.0 / 7.0 if kind == "attn_bwd" else 1)
+        alg = (2 if kind == "attn_fwd" else 4) * 2.0 * nseq * n * n * hd
+        rows.append({"kernel": "short " + kind.replace("attn_", ""), "head_dim": hd, "seq_len": n,
+                     "nseq": nseq, "launches": cnt, "total_ms": round(tot_ms, 3),
+                     "avg_ms": round(tot_ms / cnt, 4), "alg_bytes": nb,
+                     "achieved_gbs": round(nb / avg_s / 1e9, 1),
+                     "frac": round(nb / avg_s / 1e9 / PEAK_HBM_GBS, 4),
+                     "executed_over_algorithmic_flop": round(ex / alg, 3)})
+    rows.sort(key=lambda r: -r["total_ms"])
+    return rows
+
+
+def st_leg(args, rank, world, device):
+    """Auxiliary: the same train step in spatial_temporal mode (SURVEY D1 / BASELINE.md
+    section 2, 'build default', ~29 TFLOP per step: spatial attention per frame over its
+    H*W tokens on the flash kernels + temporal attention per pixel over its T tokens on the
+    short-sequence kernels), from the benchmark init at --lr, the headline's step indices.
+    Reports frames/s, the spatial attention units (MFMA roofline) and the temporal kernels
+    (HBM roofline, short_attention_roofline)."""
+    import copy as _copy
+    from vdiff import ops
+    from vdiff.ddp import broadcast_parameters
+    from vdiff.engine import Trainer, synthetic_clip
+    from vdiff.flops import unet_forward_work
+    from vdiff.schedulers import LinearNoiseScheduler
+    a2 = _copy.copy(args)
+    a2.mode = "spatial_temporal"
+    seed_host(1234 + rank)
+    model = build_model(a2, device)
+    broadcast_parameters(model)
+    work = unet_forward_work(model, (args.clips_per_gpu, 195, args.frames, args.size, args.size))
+    tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=args.lr)
+    clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
+    nsteps = args.steps if args.st_steps < 0 else args.st_steps
+    losses = [tr.step(clip) for _ in range(args.warmup)]
+    barrier_sync(world)
+    timer = ops.KernelTimer(attention=True, convs=False)
+    ops.set_timer(timer)
+    t0 = time.perf_counter()
+    for _ in range(nsteps):
+        losses.append(tr.step(clip))
+    barrier_sync(world)
+    el = time.perf_counter() - t0
+    ops.set_timer(None)
+    el = max_over_ranks(el, world, device)
+    ms = el / nsteps * 1e3
+    summary = timer.summary()
+    roof, _, units = pick_roofline(summary, args.dtype)
+    short = short_attention_roofline(summary)
+    step_flops = 3 * work.total * args.clips_per_gpu
+    out = {"metric": "train-step frames/sec, spatial_temporal attention (build default mode)",
+           "value": round(world * args.clips_per_gpu * args.frames * nsteps / el, 4),
+           "unit": "frames/s", "ms_per_step": round(ms, 2), "steps": nsteps,
+           "warmup": args.warmup, "train_losses": [_num(x, 5) for x in losses],
+           "fwd_tflop_per_clip": round(work.total / 1e12, 3),
+           "train_tflop_per_step": round(step_flops / 1e12, 2),
+           "model_tflops_per_gpu": round(step_flops / (el / nsteps) / 1e12, 1),
+           "roofline_spatial": roof, "attention_units": units,
+           "roofline_temporal": ({"bound": "hbm", "achieved": short[0]["achieved_gbs"],
+                                  "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": short[0]["frac"],
+                                  "kernel": f"{short[0]['kernel']} (head_dim "
+                                            f"{short[0]['head_dim']}, seq {short[0]['seq_len']},"
+                                            f" {short[0]['nseq']} seq/launch)",
+                                  "traffic": None} if short else None),
+           "temporal_kernels": short}
+    log(f"spatial_temporal: {ms:.1f} ms/step, {out['value']} frames/s")
+    for r in short:
+        log("  temporal", r)
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def _num(x, nd=4):
     """A float for the JSON line: None when not finite (NaN / Infinity are not JSON)."""
     x = float(x)
@@ -598,8 +692,11 @@ def main():
         result["model_tflops_per_gpu"] = round(step_flops / (el / args.steps) / 1e12, 1)
         # rank 0's MSE losses, warm-up then timed steps (train.py:131-132 prints them)
         result["train_losses"] = [_num(x, 5) for x in train_losses]
-        result["train_init"] = {"init": args.init, "lr": args.lr,
-                                "warmup_steps": args.warmup, "timed_steps": args.steps}
+        result["train_init"] = {"init": args.init, "lr": args.lr, "reference_lr": 1e-2,
+                                "warmup_steps": args.warmup, "timed_steps": args.steps,
+                                "note": "not the reference's hyperparameter when lr != 1e-2: "
+                                        "train.py:102 trains at 1e-2, where this init's loss "
+                                        "diverges within 25 steps (DESIGN section 5)"}
         log(f"train: {ms:.1f} ms/step, {result['value']:.3f} frames/s, loss {float(loss):.4f}, "
             f"model {result['model_tflops_per_gpu']} TFLOP/s/GPU (3x fwd)")
         for r in rows:
@@ -690,6 +787,13 @@ def main():
         except Exception as e:
             log(f"xattn leg failed: {type(e).__name__}: {e}")
             result["audio_xattn"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
+
+    if args.only in ("train", "all") and args.st_steps != 0 and args.mode == "joint":
+        try:  # an auxiliary leg: never let it take the headline numbers down
+            result["spatial_temporal"] = st_leg(args, rank, world, device)
+        except Exception as e:
+            log(f"spatial_temporal leg failed: {type(e).__name__}: {e}")
+            result["spatial_temporal"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
 
     if args.only in ("train", "all") and args.train_graph and world == 1:
         try:  # an auxiliary leg: never let it take the headline numbers down

@@ -306,6 +306,17 @@ size_t vd_attention_bwd_workspace_size(const vd_attn_desc* d);
  * (base|nb2|w8|p8|p4|d8|d8n|d4|pair|p4n2|role|sp|asm).  No reference counterpart: an A/B
  * and test hook. */
 int vd_attention_set_config(int cfg);
+/* Short sequences (bf16, seq_len <= 32, head_dim 32/64/128/256, 16-B aligned rows: the
+ * temporal attention of the spatial_temporal mode, T = 16 / 25 frames per pixel, and the
+ * ViViT encoder's 9 tokens) run on dedicated kernels, one wave per sequence with 16x16 MFMA
+ * tiles: vd_attention_fwd / _fwd_ws, and vd_attention_bwd as ONE fused dQ / dK / dV kernel
+ * (no workspace used).  vd_attention_short_path(d) says whether d takes that path;
+ * vd_attention_set_short(0) (or env VDIFF_ATTN_SHORT=0) routes such shapes to the flash
+ * kernels instead (A/B and test hook; returns the previous setting).  No reference
+ * counterpart: the reference materialises T x T scores (unet.py:361-365 per regrouped
+ * sequence). */
+int vd_attention_short_path(const vd_attn_desc* d);
+int vd_attention_set_short(int on);
 /* dout uses the o_* strides; dq/dk/dv use the q/k/v strides (so they can be
  * written straight into a d(qkv) buffer) and are OVERWRITTEN. */
 int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k,

@@ -2704,6 +2704,25 @@ size_t bwd_ws_any(const vd_attn_desc* d, int nkv, bool cross) {
 
 }  // namespace
 
+namespace vd {
+bool short_attn_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                   const void* o);
+int short_attn_fwd(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
+                   float* lse, hipStream_t st);
+int short_attn_bwd(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                   const void* o, const void* dout, const float* lse, void* dq, void* dk,
+                   void* dv, hipStream_t st);
+}  // namespace vd
+
+namespace {
+// the short-sequence kernels (attn_short.hip) for seq_len <= 32; VDIFF_ATTN_SHORT=0 or
+// vd_attention_set_short(0) routes those shapes to the flash kernels (A/B, tests)
+std::atomic<int> g_short{[] {
+  const char* e = std::getenv("VDIFF_ATTN_SHORT");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+}  // namespace
+
 extern "C" {
 
 #ifdef VD_ATTN_STAMPS
@@ -2722,9 +2741,19 @@ int vd_attention_fwd_ws(const vd_attn_desc* d, const void* q, const void* k, con
   int rc = check_attn(d);
   if (rc) return rc;
   VD_REQUIRE(q && k && v && o && lse, "null tensor");
+  if (g_short.load() && vd::short_attn_ok(d, q, k, v, o))
+    return vd::short_attn_fwd(d, q, k, v, o, lse, VD_STREAM(stream));
   return fwd_any(d, self_kv(d), false, q, k, v, o, lse, workspace, workspace_bytes,
                  VD_STREAM(stream));
 }
+
+int vd_attention_short_path(const vd_attn_desc* d) {
+  if (!d || check_attn(d)) return 0;
+  static const char kAligned[16] __attribute__((aligned(16))) = {};
+  return g_short.load() && vd::short_attn_ok(d, kAligned, kAligned, kAligned, kAligned) ? 1 : 0;
+}
+
+int vd_attention_set_short(int on) { return g_short.exchange(on ? 1 : 0); }
 
 int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
                      float* lse, void* stream) {
@@ -2771,6 +2800,10 @@ int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k, c
 int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                      const void* o, const void* dout, const float* lse, void* dq, void* dk,
                      void* dv, void* workspace, void* stream) {
+  if (g_short.load() && d && !check_attn(d) && vd::short_attn_ok(d, q, k, v, o)) {
+    VD_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv, "null tensor");
+    return vd::short_attn_bwd(d, q, k, v, o, dout, lse, dq, dk, dv, VD_STREAM(stream));
+  }
   int rc = vd_attention_bwd_dq(d, q, k, v, o, dout, lse, dq, workspace, stream);
   if (rc) return rc;
   return vd_attention_bwd_dkdv(d, q, k, v, dout, lse, dk, dv, workspace, stream);

@@ -929,10 +929,19 @@ class AttentionFn(torch.autograd.Function):
         base, obase, dobase, dbase = (qkv.data_ptr(), out.data_ptr(), dout.data_ptr(),
                                       dqkv.data_ptr())
         for (d, qo, ko, vo, oo), lse in zip(launches, lses):
-            ws = torch.empty(max(1, _lib.lib().vd_attention_bwd_workspace_size(d)),
-                             dtype=torch.uint8, device=qkv.device)
             st = _stream(qkv)
             ev = _timer.begin() if _timer is not None and _timer.attention else None
+            if _lib.lib().vd_attention_short_path(d):
+                # short sequences (temporal mode, <= 32 tokens): ONE fused dQ / dK / dV
+                # launch, no workspace (attn_short.hip)
+                _lib.call("vd_attention_bwd", d, base + qo * es, base + ko * es, base + vo * es,
+                          obase + oo * es, dobase + oo * es, _p(lse), dbase + qo * es,
+                          dbase + ko * es, dbase + vo * es, None, st)
+                if ev is not None:
+                    _timer.end(ev, "attn_bwd", d)
+                continue
+            ws = torch.empty(max(1, _lib.lib().vd_attention_bwd_workspace_size(d)),
+                             dtype=torch.uint8, device=qkv.device)
             _lib.call("vd_attention_bwd_dq", d, base + qo * es, base + ko * es, base + vo * es,
                       obase + oo * es, dobase + oo * es, _p(lse), dbase + qo * es, _p(ws), st)
             if ev is not None:

@@ -1,0 +1,118 @@
+"""Short-sequence attention (attn_short.hip: one wave per sequence of <= 32 tokens, 16x16
+MFMA tiles, a fused dQ / dK / dV backward) -- the temporal half of the spatial_temporal
+mode (T = 16 at config 2, 25 at config 4, one sequence per pixel) and the ViViT encoder's
+9-token heads -- against the oracle's materialised softmax attention (oracle.nn.qkv_attention,
+pinned to the reference QKVAttentionLegacy / QKVAttention by the golden regroupings) in fp32
+on the same bf16-rounded inputs, and against the flash kernels (vd_attention_set_short(0)).
+Bars: bf16 output rel-L2 <= 1e-2 and gradients <= 2e-2 against fp32 (P and dS are rounded to
+bf16 once, as in the flash kernels); lse within 1e-3 + 1e-4 |lse|."""
+import math
+
+import pytest
+import torch
+
+from oracle import nn as onn
+from oracle.fixtures import rel_l2, seeded
+
+from conftest import record_metric
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _run(B, C, heads, T, HW, mode, legacy, seed, amp=1.0):
+    from vdiff import ops
+    N = T * HW
+    qkv = (seeded((B, 3 * C, N), seed) * amp).bfloat16().float()
+    qr = qkv.clone().requires_grad_(True)
+    ref = onn.qkv_attention(qr, heads, legacy=legacy, mode=mode, spatial=(T, HW, 1))
+    g = seeded(ref.shape, seed + 1)
+    ref.backward(g)
+    qd = ops.to_cl(qkv.to(dev, torch.bfloat16)).requires_grad_(True)
+    out = ops.attention(qd, heads=heads, mode=mode, spatial=(T, HW, 1), legacy=legacy)
+    out.backward(ops.to_cl(g.to(dev, torch.bfloat16)))
+    return rel_l2(out, ref), rel_l2(qd.grad, qr.grad), out.detach(), qd.grad.detach()
+
+
+def _uses_short(B, C, heads, T, HW, mode, legacy):
+    from vdiff import _lib, ops
+    d = ops._attn_desc(B, T * HW, C, heads, C // heads, mode, (T, HW, 1), _lib.VD_BF16, legacy)
+    return all(_lib.lib().vd_attention_short_path(x[0]) for x in d)
+
+
+@pytest.mark.parametrize("C", [64, 128, 256])
+@pytest.mark.parametrize("T", [16, 25])
+def test_temporal_bf16_vs_oracle(C, T):
+    """The temporal mode at the two BASELINE frame counts and the three level widths."""
+    B, HW = 2, 48
+    assert _uses_short(B, C, 1, T, HW, "temporal", True)
+    e_o, e_g, _, _ = _run(B, C, 1, T, HW, "temporal", True, 100 + C + T)
+    record_metric(test="short_attention_temporal", C=C, T=T, out=e_o, grad=e_g)
+    assert e_o < 1e-2 and e_g < 2e-2, (e_o, e_g)
+
+
+@pytest.mark.parametrize("T", [1, 2, 5, 9, 15, 17, 31, 32])
+def test_ragged_lengths(T):
+    """Every padding case of the 16 / 32-token tiles: masked keys, masked queries."""
+    e_o, e_g, _, _ = _run(1, 64, 1, T, 37, "temporal", True, 200 + T)
+    assert e_o < 1e-2 and e_g < 2e-2, (T, e_o, e_g)
+
+
+@pytest.mark.parametrize("legacy", [True, False])
+def test_multi_head_and_joint_short(legacy):
+    """Heads as sequence groups (QKVAttentionLegacy and QKVAttention orders), and joint mode
+    over 9 tokens with 8 heads of 32 channels (the ViViT encoder's attention shape)."""
+    e_o, e_g, _, _ = _run(2, 128, 2, 16, 20, "temporal", legacy, 300)
+    assert e_o < 1e-2 and e_g < 2e-2, (e_o, e_g)
+    assert _uses_short(16, 256, 8, 1, 9, "joint", legacy)
+    e_o, e_g, _, _ = _run(16, 256, 8, 1, 9, "joint", legacy, 301)
+    assert e_o < 1e-2 and e_g < 2e-2, (e_o, e_g)
+
+
+def test_large_logits_and_lse():
+    """Peaked softmax (|logit| up to ~60): the max subtraction, and the saved lse against
+    the fp32 log-sum-exp."""
+    from vdiff import _lib, ops
+    B, C, T, HW = 1, 64, 16, 64
+    e_o, e_g, _, _ = _run(B, C, 1, T, HW, "temporal", True, 400, amp=4.0)
+    assert e_o < 1e-2 and e_g < 3e-2, (e_o, e_g)
+    qkv = (seeded((B, 3 * C, T * HW), 401) * 3.0).bfloat16()
+    x = ops.to_cl(qkv.to(dev))
+    (d, qo, ko, vo, oo), = ops._attn_desc(B, T * HW, C, 1, C, "temporal", (T, HW, 1),
+                                          _lib.VD_BF16, True)
+    out = ops.empty_cl([B, C, T * HW], torch.bfloat16, dev)
+    lse = torch.empty(d.nseq * d.seq_len, dtype=torch.float32, device=dev)
+    base = x.data_ptr()
+    _lib.call("vd_attention_fwd_ws", d, base + qo * 2, base + ko * 2, base + vo * 2,
+              out.data_ptr(), lse.data_ptr(), None, 0, torch.cuda.current_stream().cuda_stream)
+    q, k, _ = qkv.float().reshape(B, 3, C, T, HW).unbind(1)
+    s = torch.einsum("ctp,cup->ptu", q[0], k[0]) / math.sqrt(C)   # [pixel, query t, key u]
+    ref = torch.logsumexp(s, dim=-1).reshape(-1)
+    err = (lse.cpu() - ref).abs()
+    assert bool((err <= 1e-3 + 1e-4 * ref.abs()).all()), float(err.max())
+
+
+def test_short_equals_flash_kernels():
+    """The same temporal launch on the short kernels and on the flash kernels (the previous
+    path, vd_attention_set_short(0)): two bf16 evaluations of one fp32 reference."""
+    from vdiff import _lib
+    lib = _lib.lib()
+    prev = lib.vd_attention_set_short(0)
+    try:
+        _, _, o_f, g_f = _run(2, 64, 1, 16, 40, "temporal", True, 500)
+    finally:
+        lib.vd_attention_set_short(prev)
+    _, _, o_s, g_s = _run(2, 64, 1, 16, 40, "temporal", True, 500)
+    assert rel_l2(o_s.float(), o_f.float()) < 1e-2
+    assert rel_l2(g_s.float(), g_f.float()) < 2e-2
+
+
+def test_short_path_predicate():
+    """vd_attention_short_path: bf16 with <= 32 tokens only; fp32 (parity mode) and longer
+    sequences keep the flash kernels."""
+    from vdiff import _lib, ops
+    lib = _lib.lib()
+    for T, dt, want in ((16, _lib.VD_BF16, 1), (32, _lib.VD_BF16, 1), (33, _lib.VD_BF16, 0),
+                        (16, _lib.VD_F32, 0)):
+        (d, *_), = ops._attn_desc(1, T * 8, 64, 1, 64, "temporal", (T, 8, 1), dt, True)
+        assert lib.vd_attention_short_path(d) == want, (T, dt)
