@@ -235,16 +235,17 @@ class Stream:
 
 # Code placement (MI355X_MICROARCH.md "Two waves per SIMD" item 8: a hand-written stream can
 # lose ~13 % under a uniform 4-byte shift): kernels named here start with one s_nop 0, which
-# shifts their whole instruction stream by 4 bytes.  VDIFF_ASM_PHASE (A/B builds,
-# tools/build_asm_phase.sh): "all", or a comma list of kernel names, flips the phase of those
-# kernels relative to this table.
+# shifts their whole instruction stream by 4 bytes.  PHASE_FLIP (A/B builds only:
+# gen_attn_asm.py --phase=..., tools/build_asm_phase.sh): "all", or a comma list of kernel
+# names, flips the phase of those kernels relative to this table.  The product build (make)
+# never sets it, and nothing here reads the environment, so a leftover variable cannot
+# shift the shipped code (advisor r04).
 PHASE4 = set()
+PHASE_FLIP = ""
 
 
 def _phase4(name):
-    import os
-    env = os.environ.get("VDIFF_ASM_PHASE", "")
-    flip = env == "all" or name in env.split(",")
+    flip = PHASE_FLIP == "all" or name in PHASE_FLIP.split(",")
     return (name in PHASE4) != flip
 
 

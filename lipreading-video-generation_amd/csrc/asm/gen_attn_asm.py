@@ -480,6 +480,10 @@ def gen_dq(probe=None):
 
 def main():
     out = sys.argv[1]
+    for arg in sys.argv[2:]:  # A/B code-placement builds only (tools/build_asm_phase.sh)
+        if arg.startswith("--phase="):
+            import asmgen
+            asmgen.PHASE_FLIP = arg[len("--phase="):]
     from gen_d128 import gen_dkdv128, gen_dq128
     from gen_fwd128 import gen_fwd128
     from gen_fwd import gen_fwd

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an A/B variant of libvdiff.so whose hand-scheduled attention kernels start 4 bytes later
-# (VDIFF_ASM_PHASE, asm/asmgen.py PHASE4):
+# (gen_attn_asm.py --phase=..., asm/asmgen.py PHASE4 / PHASE_FLIP):
 #   tools/build_asm_phase.sh NAME "all" | "kernel,kernel"  ->  vdiff/libvdiff_NAME.so
 # Run it with VDIFF_LIB=<that path>.  Experiments only; the product build is make.
 set -e
@@ -9,7 +9,7 @@ make -s -j8 >/dev/null
 NAME=$1; PH=$2
 T=$(mktemp -d)
 mkdir -p $T/build
-VDIFF_ASM_PHASE=$PH python3 asm/gen_attn_asm.py $T/attn_asm.s
+python3 asm/gen_attn_asm.py $T/attn_asm.s --phase=$PH
 /opt/rocm/llvm/bin/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=gfx950 -c $T/attn_asm.s -o $T/attn_asm.co.o
 /opt/rocm/llvm/bin/ld.lld -shared $T/attn_asm.co.o -o $T/attn_asm.hsaco
 python3 asm/blob.py $T/attn_asm.hsaco $T/build/attn_asm_blob.inc vd_attn_asm_hsaco
