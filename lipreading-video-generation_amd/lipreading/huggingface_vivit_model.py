@@ -9,7 +9,9 @@ Y_test_p globals (set by main.py, :38-41); the one-argument call
 arguments, with the same shapes (N x 5 x 1 x 32 x 32 clips, integer labels).  Differences: data are moved to the GPU
 once per epoch-batch as in the reference, `best_model_wts` uses copy.deepcopy (the
 reference imports `deepcopy` but calls `copy.deepcopy`, :90, a NameError), and the
-validation loss is computed rather than reusing the last training loss (:80-84).
+validation loss is computed rather than reusing the last training loss (:80-84).  Training
+accuracy counts the train-mode predictions of each step's own forward, as the reference
+does (:52-64).
 """
 from __future__ import annotations
 
@@ -58,11 +60,9 @@ def train_huggingface_model(VIVIT, X_train=None, Y_train=None, X_test=None, Y_te
             labels = Y_train[i:i + batch_size].to(device)
             loss = tr.step(data, labels)
             run_loss += float(loss) * len(labels)
+            # training accuracy from the step's own train-mode predictions (:52-64)
+            run_ok += int((tr.logits.argmax(1) == labels).sum())
         VIVIT.eval()
-        with torch.no_grad():
-            for i in range(0, len(X_train), batch_size):
-                out = VIVIT(X_train[i:i + batch_size].to(device))
-                run_ok += int((out.argmax(1).cpu() == Y_train[i:i + batch_size]).sum())
         log(f"train loss is {run_loss / len(X_train)}, epoch_acc is {run_ok / len(X_train)}")
         val_loss, val_ok = 0.0, 0
         with torch.no_grad():

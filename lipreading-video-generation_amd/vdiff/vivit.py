@@ -287,7 +287,9 @@ class VivitTrainer:
 
     def _fwd_bwd(self, x, y):
         self.model.train()
-        loss = F.cross_entropy(self.model(x), y)
+        out = self.model(x)
+        self.logits = out.detach()  # the step's train-mode predictions (graph: static buffer)
+        loss = F.cross_entropy(out, y)
         loss.backward()
         return loss.detach()
 
@@ -352,6 +354,7 @@ class VivitTrainer:
     def _step(self, data, labels, zero=True):
         self.model.train()
         out = self.model(data)
+        self.logits = out.detach()  # the step's train-mode predictions (graph: static buffer)
         loss = F.cross_entropy(out, labels)
         loss.backward()
         if self.bucketer is not None:
