@@ -19,3 +19,6 @@ case $rc in 0|1) ;; *) echo "pytest rc=$rc: stopping"; exit $rc;; esac
 timeout -k 10 600 python3 -u bench.py --steps 5 --warmup 2 --c4-steps 1 --vivit-steps 5 --no-cpu \
   > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { echo "bench rc=$?"; tail -20 gpurun_out/${T}_bench.err; exit 1; }
 grep -E "spatial_temporal|temporal|train:" gpurun_out/${T}_bench.err | cut -c1-400
+timeout -k 10 200 python3 -u tools/graph_reduce_repro.py --check-grads --host-ops 3 --probe-sem \
+  > gpurun_out/${T}_repro_sem.txt 2>&1 || { echo "repro rc=$?"; tail -5 gpurun_out/${T}_repro_sem.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/${T}_repro_sem.txt | cut -c1-2500
