@@ -177,7 +177,8 @@ def test_vivit_graph_step_matches_eager():
     the bench's config-5 leg times at N = 1) against the eager step from the same weights
     (fp32), step by step: the graph's OWN captured loss (static_loss, read after each replay)
     equals the eager loss to 1e-6 at every one of six steps, and every parameter after the
-    last step agrees to 1e-6 rel-L2.  The capture's three warm-up updates are undone by
+    last step agrees to 1e-6 rel-L2 (the key biases, whose exact gradient is zero, within
+    AdamW's largest displacement).  The capture's three warm-up updates are undone by
     _restore (weights and AdamW moments), so the first replay is the first update.  The
     captured graph holds no memset node."""
     from vdiff.vivit import VivitTrainer
@@ -195,12 +196,24 @@ def test_vivit_graph_step_matches_eager():
             losses.append(float(tr.step(x, y)))   # graph: static_loss after the replay
         runs.append((losses, [p.detach().clone() for p in m.parameters()], tr))
     (le, we, _), (lg, wg, tg) = runs
+    names = [n for n, _ in tg.model.named_parameters()]
+    # the key projection's bias has an exactly zero gradient (softmax is invariant to a
+    # per-query constant, q.(k_j + b) = q.k_j + q.b): its fp32 gradient is rounding noise
+    # that AdamW's g / (sqrt(v) + eps) turns into steps of up to lr, whose signs differ
+    # between the eager and the captured AdamW arithmetic (round 5: 2e-4 rel-L2 after six
+    # steps, tools/vivit_graph_diff.py); it is held to the largest displacement AdamW allows
+    noise = [i for i, n in enumerate(names) if n.endswith("attention.k_proj.bias")]
+    errs = {n: rel_l2(a, b) for n, a, b in zip(names, wg, we)}
     record_metric(test="vivit_graph_vs_eager", losses_eager=le, losses_graph=lg,
-                  max_weight_rel_l2=max(rel_l2(a, b) for a, b in zip(wg, we)))
+                  max_weight_rel_l2=max(v for i, v in enumerate(errs.values()) if i not in noise),
+                  k_proj_bias_rel_l2=max(errs[names[i]] for i in noise))
     for i, (a, b) in enumerate(zip(lg, le)):
         assert abs(a - b) <= 1e-6 * abs(b), (i, lg, le)
-    for a, b in zip(wg, we):
-        assert rel_l2(a, b) <= 1e-6
+    for i, (n, a, b) in enumerate(zip(names, wg, we)):
+        if i in noise:
+            assert float((a - b).abs().max()) <= 2 * 6 * 1e-4, n
+        else:
+            assert errs[n] <= 1e-6, (n, errs[n])
     types = tg.node_types()
     assert types.get("memset", 0) == 0 and types.get("kernel", 0) > 50, types
 
