@@ -15,16 +15,51 @@ def short(name: str) -> str:
     return name.replace("unsigned short", "bf16").replace("void ", "")
 
 
-def from_db(path):
+def _grid_cols(c):
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    for cand in (("grid_size_x", "grid_size_y", "grid_size_z"), ("grid_x", "grid_y", "grid_z"),
+                 ("grid_size",)):
+        if all(x in cols for x in cand):
+            return cand
+    return ()
+
+
+def from_db(path, by_grid=False):
+    """{kernel: [calls, total ns, min, max]}; by_grid: keyed (kernel, grid) instead."""
     c = sqlite3.connect(path)
+    g = _grid_cols(c) if by_grid else ()
+    sel = ", ".join(("name", "duration") + g)
     rows = {}
-    for name, dur in c.execute("select name, duration from kernels"):
-        r = rows.setdefault(short(name), [0, 0, float("inf"), 0])
+    for rec in c.execute(f"select {sel} from kernels"):
+        key = short(rec[0]) if not by_grid else (short(rec[0]), tuple(rec[2:]))
+        r = rows.setdefault(key, [0, 0, float("inf"), 0])
         r[0] += 1
-        r[1] += dur
-        r[2] = min(r[2], dur)
-        r[3] = max(r[3], dur)
+        r[1] += rec[1]
+        r[2] = min(r[2], rec[1])
+        r[3] = max(r[3], rec[1])
     return rows
+
+
+def unit_line(path):
+    """The bench's roofline unit (the head_dim-64 backward pair at N = 262144, one sequence per
+    launch: 8 N^2 D algorithmic FLOP) from the launches of ONE grid shape per kernel -- the
+    grid with the largest total time (the headline's N = 262144 launches; the auxiliary
+    spatial_temporal leg runs the same kernels per frame at N = 16384 on other grids)."""
+    rows = from_db(path, by_grid=True)
+    best = {}
+    for (name, grid), r in rows.items():
+        if name in ("vd_attn_bwd_dq_d64", "vd_attn_bwd_dkdv_d64"):
+            if name not in best or r[1] > best[name][1][1]:
+                best[name] = (grid, r)
+    if len(best) < 2:
+        return None
+    (gq, dq), (gk, dkdv) = best["vd_attn_bwd_dq_d64"], best["vd_attn_bwd_dkdv_d64"]
+    unit_us = dq[1] / dq[0] / 1e3 + dkdv[1] / dkdv[0] / 1e3
+    flop = 8.0 * 262144 ** 2 * 64
+    return (f"D = 64 backward unit (grids dq {gq} x{dq[0]}, dk/dv {gk} x{dkdv[0]}): "
+            f"{unit_us / 1e3:.3f} ms = {flop / (unit_us * 1e-6) / 1e12:.1f} TFLOP/s algorithmic "
+            f"= frac {flop / (unit_us * 1e-6) / 2.5e15:.4f} of 2.5 PF/s (every launch of that "
+            f"grid in the process, warm-up steps included)")
 
 
 def from_csv(path):
@@ -47,16 +82,18 @@ def main(path):
               f"{mx / 1e3:.1f} | {100 * tot / total:.2f} |")
     print(f"\nTotal kernel time: {total / 1e6:.3f} ms over {sum(r[0] for r in rows.values())} "
           f"dispatches")
-    # the bench's roofline unit (the head_dim-64 backward pair at N = 262144, one sequence per
-    # launch: 8 N^2 D algorithmic FLOP) from these averages, to set beside roofline.frac
-    dq, dkdv = rows.get("vd_attn_bwd_dq_d64"), rows.get("vd_attn_bwd_dkdv_d64")
-    if dq and dkdv:
-        unit_us = dq[1] / dq[0] / 1e3 + dkdv[1] / dkdv[0] / 1e3
-        flop = 8.0 * 262144 ** 2 * 64
-        print(f"\nD = 64 backward unit from these averages: {unit_us / 1e3:.3f} ms = "
-              f"{flop / (unit_us * 1e-6) / 1e12:.1f} TFLOP/s algorithmic = "
-              f"frac {flop / (unit_us * 1e-6) / 2.5e15:.4f} of 2.5 PF/s "
-              f"(every launch of the process, warm-up and auxiliary legs included)")
+    if path.endswith(".db"):
+        g = from_db(path, by_grid=True)
+        print("\nHand-scheduled attention kernels by grid shape (the headline's joint launches "
+              "and the auxiliary legs' per-frame / per-clip launches apart):\n")
+        print("| kernel | grid | calls | total ms | avg us |")
+        print("|---|---|---:|---:|---:|")
+        for (name, grid), (n, tot, _, _) in sorted(g.items(), key=lambda kv: -kv[1][1]):
+            if name.startswith("vd_attn_"):
+                print(f"| `{name}` | {grid} | {n} | {tot / 1e6:.3f} | {tot / n / 1e3:.1f} |")
+        line = unit_line(path)
+        if line:
+            print("\n" + line)
 
 
 if __name__ == "__main__":
