@@ -188,7 +188,7 @@ def _pmc_traffic(keys):
     return None if any(v is None for v in vals) else sum(vals)
 
 
-def pick_roofline(summary, dtype):
+def pick_roofline(summary, dtype, pmc=True):
     """Per-kernel executed rates, then per-UNIT algorithmic rates: unit "fwd"
     = one forward launch (2 products); unit "bwd" = the dQ + dK/dV launch pair (4
     products: backward = 2x forward, recompute not credited).  The roofline object is the
@@ -197,6 +197,8 @@ def pick_roofline(summary, dtype):
     peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
     rows, kern = [], {}
     for (kind, hd, n, nseq), (cnt, tot_ms) in summary.items():
+        if n <= 32:  # the short-sequence kernels are HBM-bound: short_attention_roofline
+            continue
         f = attention_kernel_flops(kind, n, hd, nseq)
         avg_s = tot_ms / cnt / 1e3
         kern[(kind, hd, n, nseq)] = (cnt, tot_ms)
@@ -232,7 +234,8 @@ def pick_roofline(summary, dtype):
         return None, rows, units
     top = units[0]
     names = ["attn_fwd"] if top["unit"] == "fwd" else ["attn_bwd_dq", "attn_bwd_dkdv"]
-    traffic = _pmc_traffic([f"{k}_d{top['head_dim']}" for k in names])
+    # the committed PMC rows are per-launch bytes at the headline's joint shapes
+    traffic = _pmc_traffic([f"{k}_d{top['head_dim']}" for k in names]) if pmc else None
     roof = {"bound": "mfma", "achieved": top["tflops"], "peak": peak, "unit": "TFLOP/s",
             "frac": top["frac"], "traffic": traffic, "executed_frac": top["executed_frac"],
             "kernel": f"{top['kernels']} (head_dim {top['head_dim']}, seq {top['seq_len']}, "
@@ -492,7 +495,7 @@ def st_leg(args, rank, world, device):
     el = max_over_ranks(el, world, device)
     ms = el / nsteps * 1e3
     summary = timer.summary()
-    roof, _, units = pick_roofline(summary, args.dtype)
+    roof, _, units = pick_roofline(summary, args.dtype, pmc=False)
     short = short_attention_roofline(summary)
     step_flops = 3 * work.total * args.clips_per_gpu
     out = {"metric": "train-step frames/sec, spatial_temporal attention (build default mode)",
@@ -508,7 +511,9 @@ def st_leg(args, rank, world, device):
                                   "kernel": f"{short[0]['kernel']} (head_dim "
                                             f"{short[0]['head_dim']}, seq {short[0]['seq_len']},"
                                             f" {short[0]['nseq']} seq/launch)",
-                                  "traffic": None} if short else None),
+                                  "traffic": _pmc_traffic([short[0]["kernel"].replace(
+                                      "short ", "short_attn_") + f"_d{short[0]['head_dim']}"])}
+                                 if short else None),
            "temporal_kernels": short}
     log(f"spatial_temporal: {ms:.1f} ms/step, {out['value']} frames/s")
     for r in short:

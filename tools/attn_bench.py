@@ -28,27 +28,34 @@ def check():
         assert e < 2e-2
 
 
-def bench(C, N, reps, bwd=True):
+def bench(C, N, reps, bwd=True, mode="joint", T=16):
+    """mode "temporal": the spatial_temporal mode's per-pixel sequences of T frames over the
+    N = T * HW tokens of a clip (the short-sequence kernels, HBM-bound: GB/s reported)."""
+    from vdiff.flops import short_attention_bytes
+    sp = (T, N // T, 1) if mode != "joint" else None
     qkv = ops.to_cl(torch.randn(1, 3 * C, N, device="cuda", dtype=torch.bfloat16))
     qkv.requires_grad_(True)
     g = ops.to_cl(torch.randn(1, C, N, device="cuda", dtype=torch.bfloat16))
     for _ in range(1):
-        out = ops.attention(qkv, 1)
+        out = ops.attention(qkv, 1, mode=mode, spatial=sp)
         if bwd:
             out.backward(g)
     torch.cuda.synchronize()
     timer = ops.KernelTimer()
     ops.set_timer(timer)
     for _ in range(reps):
-        out = ops.attention(qkv, 1)
+        out = ops.attention(qkv, 1, mode=mode, spatial=sp)
         if bwd:
             out.backward(g)
     ops.set_timer(None)
     for (kind, hd, n, nseq), (cnt, tot) in sorted(timer.summary().items()):
         f = attention_kernel_flops(kind, n, hd, nseq)
         avg = tot / cnt
-        print(f"{kind:14s} d={hd:3d} N={n:6d}: {avg:8.3f} ms  {f / avg / 1e9:7.1f} TF/s "
-              f"({f / avg / 1e9 / 2500 * 100:5.1f}% of 2.5 PF)", flush=True)
+        extra = ""
+        if n <= 32:
+            extra = f"  {short_attention_bytes(kind, n, hd, nseq) / avg / 1e6:7.1f} GB/s"
+        print(f"{kind:14s} d={hd:3d} N={n:6d} x{nseq}: {avg:8.3f} ms  {f / avg / 1e9:7.1f} TF/s "
+              f"({f / avg / 1e9 / 2500 * 100:5.1f}% of 2.5 PF){extra}", flush=True)
 
 
 CALIB_ELEMS = 1 << 27   # bf16 elements per operand: 256 MiB each, past the 256 MiB L3
@@ -79,7 +86,13 @@ if __name__ == "__main__":
         sys.argv.remove("--nocheck")
     else:
         check()
+    temporal = "--temporal" in sys.argv  # the short-sequence kernels (spatial_temporal mode)
+    if temporal:
+        sys.argv.remove("--temporal")
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     for C, N in ((64, 262144), (128, 65536), (256, 16384)):
         if only is None or C == only:
-            bench(C, N, reps)
+            if temporal:
+                bench(C, N, reps, mode="temporal")
+            else:
+                bench(C, N, reps)

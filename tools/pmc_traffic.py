@@ -26,7 +26,13 @@ _VARIANT = re.compile(r"_(pipe|defer|pair)$")  # kernel variants share the launc
 _ASM = re.compile(r"^vd_(attn_\w+)_d(\d+)$")   # hand-scheduled kernels (asm/gen_attn_asm.py)
 
 
+_SHORT = re.compile(r"short_attn_(fwd|bwd)_kernel<(\d+)")  # attn_short.hip (temporal mode)
+
+
 def kernel_key(name: str) -> str:
+    m = _SHORT.search(name)
+    if m:
+        return f"short_attn_{m.group(1)}_d{m.group(2)}"
     m = _ASM.match(name)
     if m:
         return f"{m.group(1)}_d{m.group(2)}"
