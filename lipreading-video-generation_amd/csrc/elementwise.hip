@@ -459,60 +459,122 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int Co, int Ci, 
   }
 }
 
-// vd_conv_pack_weights: the jobs' outputs concatenated into one index space; each block
-// stages the jobs' start offsets in LDS.  The step's conv operands in one launch.  Each thread packs 8 consecutive output elements
-// (one 16-B bf16 store): the job is found once per 8-vector (binary search over the LDS copy
-// of the start offsets), its (outer, tap, inner) coordinates with 32-bit arithmetic once per
-// vector, and the 8 source reads walk the inner index (ci, or co when transposed) with the
-// source stride `taps` (the L2 serves the re-reads of the next taps).  A vector that does not
-// lie inside one job's 8-aligned inner run takes the per-element path.  Round 4's form
-// (64-bit divisions and a search per ELEMENT) took 0.69 ms per train step.
-template <typename T>
-__device__ __forceinline__ float pack_src(const vd_pack_desc& d, int o, int tap, int inner) {
-  const int co = d.transpose ? inner : o, ci = d.transpose ? o : inner;
-  return (co < d.Co && ci < d.Ci) ? d.w[((int64_t)co * d.Ci + ci) * d.taps + tap] : 0.f;
+// vd_conv_pack_weights: the step's conv operands in one launch, as LDS-tiled transposes.
+// A tile is 4 output channels x 64 input channels (the [Co][taps][Ci] layout) or 8 input
+// channels x 64 output channels (the transposed [Ci][taps][Co] layout), all taps: the source
+// rows w[co][ci0 ..][0 .. taps) are read contiguously (fp32), transposed in LDS, and the
+// destination rows of 64 channels written as 16-B vectors.  Every block derives the jobs' tile
+// counts and their prefix sums itself (the descriptors live on the device) and walks the
+// tiles grid-stride.  A job with more than kPackMaxTaps taps (none in the UNet) is packed
+// element by element in blocks of 2048 outputs.  Round 4's element-wise form (64-bit index
+// math and a job search per element, strided reads) took 0.69 ms per train step.
+constexpr int kPackMaxTaps = 27;
+constexpr int kPackSmem = 8 * kPackMaxTaps * 64 * 4;  // the transposed tile, the larger one
+
+__device__ __forceinline__ int pack_tiles(const vd_pack_desc& d) {
+  if (d.taps > kPackMaxTaps) return (int)((d.transpose ? (int64_t)d.Cip * d.taps * d.Cop
+                                                       : (int64_t)d.Co * d.taps * d.Cip) +
+                                          2047) / 2048;
+  return d.transpose ? ((d.Cip + 7) / 8) * ((d.Cop + 63) / 64)
+                     : ((d.Co + 3) / 4) * ((d.Cip + 63) / 64);
 }
 
 template <typename T>
 __global__ void __launch_bounds__(kBlock) pack_weights_kernel(
-    const vd_pack_desc* __restrict__ descs, int n, int64_t total) {
-  __shared__ int64_t start[1025];
-  for (int j = threadIdx.x; j < n; j += blockDim.x) start[j] = descs[j].start;
-  if (threadIdx.x == 0) start[n] = total;
+    const vd_pack_desc* __restrict__ descs, int n) {
+  extern __shared__ __attribute__((aligned(16))) float ptile[];
+  __shared__ int tstart[1025];
+  // tstart[j + 1] = the jobs' tile counts, then an inclusive Hillis-Steele scan over them
+  // (parallel: a serial walk over the descriptors costs a global-load latency per job)
+  if (threadIdx.x == 0) tstart[0] = 0;
+  for (int j = threadIdx.x; j < n; j += kBlock) tstart[j + 1] = pack_tiles(descs[j]);
   __syncthreads();
-  const int64_t nv = (total + 7) / 8;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv;
-       v += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i0 = 8 * v;
+  for (int off = 1; off < n; off <<= 1) {
+    int v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = threadIdx.x + k * kBlock + 1;
+      v[k] = (j <= n && j - off >= 1) ? tstart[j - off] : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = threadIdx.x + k * kBlock + 1;
+      if (j <= n) tstart[j] += v[k];
+    }
+    __syncthreads();
+  }
+  const int ntiles = tstart[n];
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     int lo = 0, hi = n - 1;
-    while (lo < hi) {  // the last job whose start <= i0
+    while (lo < hi) {  // the last job whose first tile <= t
       const int mid = (lo + hi + 1) >> 1;
-      if (start[mid] <= i0) lo = mid; else hi = mid - 1;
+      if (tstart[mid] <= t) lo = mid; else hi = mid - 1;
     }
     const vd_pack_desc d = descs[lo];
-    const int e0 = (int)(i0 - start[lo]);
-    const int inner_n = d.transpose ? d.Cop : d.Cip;
-    const bool fast = (start[lo] & 7) == 0 && (inner_n & 7) == 0 && i0 + 8 <= start[lo + 1];
-    if (fast) {
-      const int in0 = e0 % inner_n, rest = e0 / inner_n;
-      const int tap = rest % d.taps, o = rest / d.taps;
-      float f[8];
+    const int lt = t - tstart[lo];
+    const int taps = d.taps;
+    T* out = (T*)d.out;
+    if (taps > kPackMaxTaps) {  // element-wise fallback
+      const int inner = d.transpose ? d.Cop : d.Cip;
+      const int64_t size = d.transpose ? (int64_t)d.Cip * taps * d.Cop
+                                       : (int64_t)d.Co * taps * d.Cip;
+      for (int64_t e = (int64_t)lt * 2048 + threadIdx.x; e < size && e < (int64_t)(lt + 1) * 2048;
+           e += kBlock) {
+        const int64_t rest = e / inner;
+        const int in = (int)(e % inner), tap = (int)(rest % taps), o = (int)(rest / taps);
+        const int co = d.transpose ? in : o, ci = d.transpose ? o : in;
+        Elem<T>::st(out + e, (co < d.Co && ci < d.Ci)
+                                 ? d.w[((int64_t)co * d.Ci + ci) * taps + tap] : 0.f);
+      }
+      continue;
+    }
+    if (!d.transpose) {  // out[co][tap][ci], tile 4 co x 64 ci
+      const int nib = (d.Cip + 63) / 64;
+      const int co0 = (lt / nib) * 4, ci0 = (lt % nib) * 64;
+      const int per = 64 * taps;
+      for (int idx = threadIdx.x; idx < 4 * per; idx += kBlock) {
+        const int c = idx / per, r = idx - c * per;
+        const int cil = r / taps, tap = r - cil * taps;
+        const bool ok = co0 + c < d.Co && ci0 + cil < d.Ci;
+        ptile[(c * taps + tap) * 64 + cil] =
+            ok ? d.w[((int64_t)(co0 + c) * d.Ci + ci0) * taps + r] : 0.f;
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < 4 * taps * 8; idx += kBlock) {
+        const int row = idx >> 3, cil = (idx & 7) * 8;
+        const int c = row / taps, tap = row - c * taps;
+        if (co0 + c < d.Co && ci0 + cil < d.Cip) {
+          float f[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] = pack_src<T>(d, o, tap, in0 + k);
-      store8((T*)d.out + e0, f);
-    } else {
-      for (int k = 0; k < 8 && i0 + k < total; ++k) {
-        const int64_t i = i0 + k;
-        int j = lo;
-        while (start[j + 1] <= i) ++j;
-        const vd_pack_desc& dj = descs[j];
-        const int e = (int)(i - start[j]);
-        const int in_n = dj.transpose ? dj.Cop : dj.Cip;
-        const int rest = e / in_n;
-        Elem<T>::st((T*)dj.out + e,
-                    pack_src<T>(dj, rest / dj.taps, rest % dj.taps, e % in_n));
+          for (int k = 0; k < 8; ++k) f[k] = ptile[row * 64 + cil + k];
+          store8(out + ((int64_t)(co0 + c) * taps + tap) * d.Cip + ci0 + cil, f);
+        }
+      }
+    } else {  // out[ci][tap][co], tile 8 ci x 64 co
+      const int nob = (d.Cop + 63) / 64;
+      const int ci0 = (lt / nob) * 8, co0 = (lt % nob) * 64;
+      const int per = 8 * taps;
+      for (int idx = threadIdx.x; idx < 64 * per; idx += kBlock) {
+        const int col = idx / per, r = idx - col * per;
+        const int cil = r / taps, tap = r - cil * taps;
+        const bool ok = co0 + col < d.Co && ci0 + cil < d.Ci;
+        ptile[(cil * taps + tap) * 64 + col] =
+            ok ? d.w[((int64_t)(co0 + col) * d.Ci + ci0) * taps + r] : 0.f;
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < 8 * taps * 8; idx += kBlock) {
+        const int row = idx >> 3, col = (idx & 7) * 8;
+        const int cil = row / taps, tap = row - cil * taps;
+        if (ci0 + cil < d.Cip && co0 + col < d.Cop) {
+          float f[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = ptile[row * 64 + col + k];
+          store8(out + ((int64_t)(ci0 + cil) * taps + tap) * d.Cop + co0 + col, f);
+        }
       }
     }
+    __syncthreads();  // the tile buffer is reused by the next tile
   }
 }
 
@@ -712,8 +774,8 @@ int vd_conv_pack_weights(const vd_pack_desc* descs, int n, int64_t total, int dt
                          void* stream) {
   VD_REQUIRE(descs && n > 0 && n <= 1024 && total > 0, "bad pack job list");
   return VD_DISPATCH_DTYPE(dtype, Tp, {
-    pack_weights_kernel<Tp><<<grid_for(vd_cdiv(total, 8)), kBlock, 0, VD_STREAM(stream)>>>(
-        descs, n, total);
+    (void)total;
+    pack_weights_kernel<Tp><<<2048, kBlock, kPackSmem, VD_STREAM(stream)>>>(descs, n);
   });
 }
 

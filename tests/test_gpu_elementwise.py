@@ -260,3 +260,33 @@ def test_mse_loss_mixed_dtype_and_layout():
     pc = ops.to_cl(x)
     assert abs(float(ops.mse_loss(pc, e)) - float(torch.nn.functional.mse_loss(x, e))) <= \
         1e-6 * float(torch.nn.functional.mse_loss(x, e))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_conv_pack_weights_batched_equals_per_job(dtype):
+    """vd_conv_pack_weights (one launch, LDS-tiled transposes) against vd_conv_pack_weight
+    per job, bit for bit: ragged channel counts (195 -> 200 padded, 3 -> 8), 27 / 9 / 1
+    taps, both layouts, and a 512-tap job (the element-wise fallback)."""
+    import numpy as np
+    from vdiff import _lib, ops
+    jobs = [(64, 195, 27, 0), (64, 195, 27, 1), (3, 64, 27, 0), (3, 64, 27, 1), (256, 512, 1, 0),
+            (256, 512, 1, 1), (130, 70, 9, 0), (130, 70, 9, 1), (16, 4, 512, 0), (16, 4, 512, 1)]
+    desc = np.dtype([("w", "<u8"), ("out", "<u8"), ("Co", "<i4"), ("Ci", "<i4"), ("taps", "<i4"),
+                     ("Cip", "<i4"), ("Cop", "<i4"), ("tr", "<i4"), ("start", "<i8")])
+    rows = np.zeros(len(jobs), desc)
+    ws, outs, refs, total = [], [], [], 0
+    for r, (Co, Ci, taps, tr) in enumerate(jobs):
+        Cip, Cop = (Ci + 7) // 8 * 8, (Co + 7) // 8 * 8
+        w = seeded((Co, Ci, taps), 80 + r).to(dev)
+        shape = (Cip, taps, Cop) if tr else (Co, taps, Cip)
+        out = torch.full(shape, 7.0, dtype=dtype, device=dev)
+        rows[r] = (w.data_ptr(), out.data_ptr(), Co, Ci, taps, Cip, Cop, tr, total)
+        total += out.numel()
+        ws.append(w)
+        outs.append(out)
+        refs.append(ops._pack_weight(w, Co, Ci, taps, Cip, Cop, bool(tr), dtype))
+    table = torch.from_numpy(rows.view(np.uint8).copy()).to(dev)
+    _lib.call("vd_conv_pack_weights", table.data_ptr(), len(jobs), total, _lib.VD_BF16 if
+              dtype == torch.bfloat16 else _lib.VD_F32, torch.cuda.current_stream().cuda_stream)
+    for j, (o, ref) in enumerate(zip(outs, refs)):
+        assert torch.equal(o, ref), jobs[j]
