@@ -469,7 +469,8 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int Co, int Ci, 
 // element by element in blocks of 2048 outputs.  Round 4's element-wise form (64-bit index
 // math and a job search per element, strided reads) took 0.69 ms per train step.
 constexpr int kPackMaxTaps = 27;
-constexpr int kPackSmem = 8 * kPackMaxTaps * 64 * 4;  // the transposed tile, the larger one
+constexpr int kPackRow = 65;  // LDS row of 64 channels + 1: consecutive taps on distinct banks
+constexpr int kPackSmem = 8 * kPackMaxTaps * kPackRow * 4;  // the transposed tile, the larger
 
 __device__ __forceinline__ int pack_tiles(const vd_pack_desc& d) {
   if (d.taps > kPackMaxTaps) return (int)((d.transpose ? (int64_t)d.Cip * d.taps * d.Cop
@@ -477,6 +478,57 @@ __device__ __forceinline__ int pack_tiles(const vd_pack_desc& d) {
                                           2047) / 2048;
   return d.transpose ? ((d.Cip + 7) / 8) * ((d.Cop + 63) / 64)
                      : ((d.Co + 3) / 4) * ((d.Cip + 63) / 64);
+}
+
+template <typename T, int TAPS>
+__device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* ptile) {
+  const int tp = TAPS ? TAPS : d.taps;
+  T* out = (T*)d.out;
+    if (!d.transpose) {  // out[co][tap][ci], tile 4 co x 64 ci
+      const int nib = (d.Cip + 63) / 64;
+      const int co0 = (lt / nib) * 4, ci0 = (lt % nib) * 64;
+      const int per = 64 * tp;
+      for (int idx = threadIdx.x; idx < 4 * per; idx += kBlock) {
+        const int c = idx / per, r = idx - c * per;
+        const int cil = r / tp, tap = r - cil * tp;
+        const bool ok = co0 + c < d.Co && ci0 + cil < d.Ci;
+        ptile[(c * tp + tap) * kPackRow + cil] =
+            ok ? d.w[((int64_t)(co0 + c) * d.Ci + ci0) * tp + r] : 0.f;
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < 4 * tp * 8; idx += kBlock) {
+        const int row = idx >> 3, cil = (idx & 7) * 8;
+        const int c = row / tp, tap = row - c * tp;
+        if (co0 + c < d.Co && ci0 + cil < d.Cip) {
+          float f[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = ptile[row * kPackRow + cil + k];
+          store8(out + ((int64_t)(co0 + c) * tp + tap) * d.Cip + ci0 + cil, f);
+        }
+      }
+    } else {  // out[ci][tap][co], tile 8 ci x 64 co
+      const int nob = (d.Cop + 63) / 64;
+      const int ci0 = (lt / nob) * 8, co0 = (lt % nob) * 64;
+      const int per = 8 * tp;
+      for (int idx = threadIdx.x; idx < 64 * per; idx += kBlock) {
+        const int col = idx / per, r = idx - col * per;
+        const int cil = r / tp, tap = r - cil * tp;
+        const bool ok = co0 + col < d.Co && ci0 + cil < d.Ci;
+        ptile[(cil * tp + tap) * kPackRow + col] =
+            ok ? d.w[((int64_t)(co0 + col) * d.Ci + ci0) * tp + r] : 0.f;
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < 8 * tp * 8; idx += kBlock) {
+        const int row = idx >> 3, col = (idx & 7) * 8;
+        const int cil = row / tp, tap = row - cil * tp;
+        if (ci0 + cil < d.Cip && co0 + col < d.Cop) {
+          float f[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = ptile[row * kPackRow + col + k];
+          store8(out + ((int64_t)(ci0 + cil) * tp + tap) * d.Cop + co0 + col, f);
+        }
+      }
+    }
 }
 
 template <typename T>
@@ -529,50 +581,11 @@ __global__ void __launch_bounds__(kBlock) pack_weights_kernel(
       }
       continue;
     }
-    if (!d.transpose) {  // out[co][tap][ci], tile 4 co x 64 ci
-      const int nib = (d.Cip + 63) / 64;
-      const int co0 = (lt / nib) * 4, ci0 = (lt % nib) * 64;
-      const int per = 64 * taps;
-      for (int idx = threadIdx.x; idx < 4 * per; idx += kBlock) {
-        const int c = idx / per, r = idx - c * per;
-        const int cil = r / taps, tap = r - cil * taps;
-        const bool ok = co0 + c < d.Co && ci0 + cil < d.Ci;
-        ptile[(c * taps + tap) * 64 + cil] =
-            ok ? d.w[((int64_t)(co0 + c) * d.Ci + ci0) * taps + r] : 0.f;
-      }
-      __syncthreads();
-      for (int idx = threadIdx.x; idx < 4 * taps * 8; idx += kBlock) {
-        const int row = idx >> 3, cil = (idx & 7) * 8;
-        const int c = row / taps, tap = row - c * taps;
-        if (co0 + c < d.Co && ci0 + cil < d.Cip) {
-          float f[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = ptile[row * 64 + cil + k];
-          store8(out + ((int64_t)(co0 + c) * taps + tap) * d.Cip + ci0 + cil, f);
-        }
-      }
-    } else {  // out[ci][tap][co], tile 8 ci x 64 co
-      const int nob = (d.Cop + 63) / 64;
-      const int ci0 = (lt / nob) * 8, co0 = (lt % nob) * 64;
-      const int per = 8 * taps;
-      for (int idx = threadIdx.x; idx < 64 * per; idx += kBlock) {
-        const int col = idx / per, r = idx - col * per;
-        const int cil = r / taps, tap = r - cil * taps;
-        const bool ok = co0 + col < d.Co && ci0 + cil < d.Ci;
-        ptile[(cil * taps + tap) * 64 + col] =
-            ok ? d.w[((int64_t)(co0 + col) * d.Ci + ci0) * taps + r] : 0.f;
-      }
-      __syncthreads();
-      for (int idx = threadIdx.x; idx < 8 * taps * 8; idx += kBlock) {
-        const int row = idx >> 3, col = (idx & 7) * 8;
-        const int cil = row / taps, tap = row - cil * taps;
-        if (ci0 + cil < d.Cip && co0 + col < d.Cop) {
-          float f[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = ptile[row * 64 + col + k];
-          store8(out + ((int64_t)(ci0 + cil) * taps + tap) * d.Cop + co0 + col, f);
-        }
-      }
+    switch (taps) {  // compile-time divisors (a runtime integer division costs ~40 VALU)
+      case 27: pack_tile<T, 27>(d, lt, ptile); break;
+      case 9: pack_tile<T, 9>(d, lt, ptile); break;
+      case 1: pack_tile<T, 1>(d, lt, ptile); break;
+      default: pack_tile<T, 0>(d, lt, ptile); break;
     }
     __syncthreads();  // the tile buffer is reused by the next tile
   }
