@@ -488,12 +488,26 @@ __device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* 
       const int nib = (d.Cip + 63) / 64;
       const int co0 = (lt / nib) * 4, ci0 = (lt % nib) * 64;
       const int per = 64 * tp;
-      for (int idx = threadIdx.x; idx < 4 * per; idx += kBlock) {
-        const int c = idx / per, r = idx - c * per;
-        const int cil = r / tp, tap = r - cil * tp;
-        const bool ok = co0 + c < d.Co && ci0 + cil < d.Ci;
-        ptile[(c * tp + tap) * kPackRow + cil] =
-            ok ? d.w[((int64_t)(co0 + c) * d.Ci + ci0) * tp + r] : 0.f;
+      // all of a thread's loads in flight before its LDS stores (a rolled loop waited on
+      // every HBM load in turn: 25 us per tile)
+      constexpr int NL = TAPS ? (4 * 64 * TAPS + kBlock - 1) / kBlock : 1;
+      for (int base = 0; base < 4 * per; base += NL * kBlock) {
+        float v[NL];
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+          const int idx = base + u * kBlock + threadIdx.x;
+          const int c = idx / per, r = idx - c * per;
+          const int cil = r / tp;
+          const bool ok = idx < 4 * per && co0 + c < d.Co && ci0 + cil < d.Ci;
+          v[u] = ok ? d.w[((int64_t)(co0 + c) * d.Ci + ci0) * tp + r] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+          const int idx = base + u * kBlock + threadIdx.x;
+          const int c = idx / per, r = idx - c * per;
+          const int cil = r / tp, tap = r - cil * tp;
+          if (idx < 4 * per) ptile[(c * tp + tap) * kPackRow + cil] = v[u];
+        }
       }
       __syncthreads();
       for (int idx = threadIdx.x; idx < 4 * tp * 8; idx += kBlock) {
@@ -510,12 +524,24 @@ __device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* 
       const int nob = (d.Cop + 63) / 64;
       const int ci0 = (lt / nob) * 8, co0 = (lt % nob) * 64;
       const int per = 8 * tp;
-      for (int idx = threadIdx.x; idx < 64 * per; idx += kBlock) {
-        const int col = idx / per, r = idx - col * per;
-        const int cil = r / tp, tap = r - cil * tp;
-        const bool ok = co0 + col < d.Co && ci0 + cil < d.Ci;
-        ptile[(cil * tp + tap) * kPackRow + col] =
-            ok ? d.w[((int64_t)(co0 + col) * d.Ci + ci0) * tp + r] : 0.f;
+      constexpr int NL = TAPS ? (64 * 8 * TAPS + kBlock - 1) / kBlock : 1;
+      for (int base = 0; base < 64 * per; base += NL * kBlock) {
+        float v[NL];
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+          const int idx = base + u * kBlock + threadIdx.x;
+          const int col = idx / per, r = idx - col * per;
+          const int cil = r / tp;
+          const bool ok = idx < 64 * per && co0 + col < d.Co && ci0 + cil < d.Ci;
+          v[u] = ok ? d.w[((int64_t)(co0 + col) * d.Ci + ci0) * tp + r] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+          const int idx = base + u * kBlock + threadIdx.x;
+          const int col = idx / per, r = idx - col * per;
+          const int cil = r / tp, tap = r - cil * tp;
+          if (idx < 64 * per) ptile[(cil * tp + tap) * kPackRow + col] = v[u];
+        }
       }
       __syncthreads();
       for (int idx = threadIdx.x; idx < 8 * tp * 8; idx += kBlock) {
