@@ -472,33 +472,43 @@ constexpr int kPackMaxTaps = 27;
 constexpr int kPackRow = 65;  // LDS row of 64 channels + 1: consecutive taps on distinct banks
 constexpr int kPackSmem = 8 * kPackMaxTaps * kPackRow * 4;  // the transposed tile, the larger
 
+// rows (outer channels) per tile: ~100-200 source floats per row of taps, so that a tile
+// carries enough work for its two barriers (1x1 jobs: 64 x 64 tiles)
+__host__ __device__ constexpr int pack_rows(int taps, bool transpose) {
+  return taps == 1 ? 64 : taps <= 9 ? 16 : (transpose ? 8 : 4);
+}
+
 __device__ __forceinline__ int pack_tiles(const vd_pack_desc& d) {
   if (d.taps > kPackMaxTaps) return (int)((d.transpose ? (int64_t)d.Cip * d.taps * d.Cop
                                                        : (int64_t)d.Co * d.taps * d.Cip) +
                                           2047) / 2048;
-  return d.transpose ? ((d.Cip + 7) / 8) * ((d.Cop + 63) / 64)
-                     : ((d.Co + 3) / 4) * ((d.Cip + 63) / 64);
+  // the row counts pack_tile<T, TAPS> uses: specialised 1 / 9 / 27 taps, else the 27-tap rows
+  const bool spec = d.taps == 1 || d.taps == 9 || d.taps == 27;
+  const int R = pack_rows(spec ? d.taps : kPackMaxTaps, d.transpose);
+  return d.transpose ? ((d.Cip + R - 1) / R) * ((d.Cop + 63) / 64)
+                     : ((d.Co + R - 1) / R) * ((d.Cip + 63) / 64);
 }
 
 template <typename T, int TAPS>
 __device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* ptile) {
   const int tp = TAPS ? TAPS : d.taps;
   T* out = (T*)d.out;
-    if (!d.transpose) {  // out[co][tap][ci], tile 4 co x 64 ci
+    if (!d.transpose) {  // out[co][tap][ci], tile R co x 64 ci
+      constexpr int R = pack_rows(TAPS ? TAPS : kPackMaxTaps, false);
       const int nib = (d.Cip + 63) / 64;
-      const int co0 = (lt / nib) * 4, ci0 = (lt % nib) * 64;
+      const int co0 = (lt / nib) * R, ci0 = (lt % nib) * 64;
       const int per = 64 * tp;
       // all of a thread's loads in flight before its LDS stores (a rolled loop waited on
       // every HBM load in turn: 25 us per tile)
-      constexpr int NL = TAPS ? (4 * 64 * TAPS + kBlock - 1) / kBlock : 1;
-      for (int base = 0; base < 4 * per; base += NL * kBlock) {
+      constexpr int NL = TAPS ? (R * 64 * TAPS + kBlock - 1) / kBlock : 1;
+      for (int base = 0; base < R * per; base += NL * kBlock) {
         float v[NL];
 #pragma unroll
         for (int u = 0; u < NL; ++u) {
           const int idx = base + u * kBlock + threadIdx.x;
           const int c = idx / per, r = idx - c * per;
           const int cil = r / tp;
-          const bool ok = idx < 4 * per && co0 + c < d.Co && ci0 + cil < d.Ci;
+          const bool ok = idx < R * per && co0 + c < d.Co && ci0 + cil < d.Ci;
           v[u] = ok ? d.w[((int64_t)(co0 + c) * d.Ci + ci0) * tp + r] : 0.f;
         }
 #pragma unroll
@@ -506,11 +516,11 @@ __device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* 
           const int idx = base + u * kBlock + threadIdx.x;
           const int c = idx / per, r = idx - c * per;
           const int cil = r / tp, tap = r - cil * tp;
-          if (idx < 4 * per) ptile[(c * tp + tap) * kPackRow + cil] = v[u];
+          if (idx < R * per) ptile[(c * tp + tap) * kPackRow + cil] = v[u];
         }
       }
       __syncthreads();
-      for (int idx = threadIdx.x; idx < 4 * tp * 8; idx += kBlock) {
+      for (int idx = threadIdx.x; idx < R * tp * 8; idx += kBlock) {
         const int row = idx >> 3, cil = (idx & 7) * 8;
         const int c = row / tp, tap = row - c * tp;
         if (co0 + c < d.Co && ci0 + cil < d.Cip) {
@@ -520,11 +530,12 @@ __device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* 
           store8(out + ((int64_t)(co0 + c) * tp + tap) * d.Cip + ci0 + cil, f);
         }
       }
-    } else {  // out[ci][tap][co], tile 8 ci x 64 co
+    } else {  // out[ci][tap][co], tile R ci x 64 co
+      constexpr int R = pack_rows(TAPS ? TAPS : kPackMaxTaps, true);
       const int nob = (d.Cop + 63) / 64;
-      const int ci0 = (lt / nob) * 8, co0 = (lt % nob) * 64;
-      const int per = 8 * tp;
-      constexpr int NL = TAPS ? (64 * 8 * TAPS + kBlock - 1) / kBlock : 1;
+      const int ci0 = (lt / nob) * R, co0 = (lt % nob) * 64;
+      const int per = R * tp;
+      constexpr int NL = TAPS ? (64 * R * TAPS + kBlock - 1) / kBlock : 1;
       for (int base = 0; base < 64 * per; base += NL * kBlock) {
         float v[NL];
 #pragma unroll
@@ -544,7 +555,7 @@ __device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* 
         }
       }
       __syncthreads();
-      for (int idx = threadIdx.x; idx < 8 * tp * 8; idx += kBlock) {
+      for (int idx = threadIdx.x; idx < R * tp * 8; idx += kBlock) {
         const int row = idx >> 3, col = (idx & 7) * 8;
         const int cil = row / tp, tap = row - cil * tp;
         if (ci0 + cil < d.Cip && co0 + col < d.Cop) {
