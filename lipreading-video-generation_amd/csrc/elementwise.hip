@@ -489,83 +489,60 @@ __device__ __forceinline__ int pack_tiles(const vd_pack_desc& d) {
                      : ((d.Co + R - 1) / R) * ((d.Cip + 63) / 64);
 }
 
+// One tile: NO outer rows (co, or ci when transposed) x 64 inner channels x all taps.  The
+// source of outer row o is the run w[...][inner0 ..][0 .. taps) (non-transposed: contiguous
+// 64 * taps floats of w[co]; transposed: R * taps floats of w[co][ci0 ..] for each of the
+// 64 co) -- both read as (row, r) pairs with 32-bit offsets; LDS image [o][tap][65].
 template <typename T, int TAPS>
 __device__ __forceinline__ void pack_tile(const vd_pack_desc& d, int lt, float* ptile) {
   const int tp = TAPS ? TAPS : d.taps;
-  T* out = (T*)d.out;
-    if (!d.transpose) {  // out[co][tap][ci], tile R co x 64 ci
-      constexpr int R = pack_rows(TAPS ? TAPS : kPackMaxTaps, false);
-      const int nib = (d.Cip + 63) / 64;
-      const int co0 = (lt / nib) * R, ci0 = (lt % nib) * 64;
-      const int per = 64 * tp;
-      // all of a thread's loads in flight before its LDS stores (a rolled loop waited on
-      // every HBM load in turn: 25 us per tile)
-      constexpr int NL = TAPS ? (R * 64 * TAPS + kBlock - 1) / kBlock : 1;
-      for (int base = 0; base < R * per; base += NL * kBlock) {
-        float v[NL];
+  const bool tr = d.transpose;
+  constexpr int RN = pack_rows(TAPS ? TAPS : kPackMaxTaps, false);
+  constexpr int RT = pack_rows(TAPS ? TAPS : kPackMaxTaps, true);
+  // load rows: non-transposed RN co rows of 64 * tp floats; transposed 64 co rows of RT * tp
+  const int nrows = tr ? 64 : RN;
+  const int per = tr ? RT * tp : 64 * tp;
+  const int ninner = tr ? d.Cop : d.Cip;                 // padded inner extent of the output
+  const int nib = (ninner + 63) / 64;
+  const int outer0 = (lt / nib) * (tr ? RT : RN), inner0 = (lt % nib) * 64;
+  const int co0 = tr ? inner0 : outer0, ci0 = tr ? outer0 : inner0;
+  const int rowlen = d.Ci * tp;                          // floats per co in w
+  const float* src = d.w + co0 * rowlen + ci0 * tp;      // (co0, ci0, tap 0)
+  const int ci_lim = d.Ci - ci0, co_lim = d.Co - co0;
+  constexpr int NL = 16;
+  for (int base = 0; base < nrows * per; base += NL * kBlock) {
+    float v[NL];
+    int dst[NL];
 #pragma unroll
-        for (int u = 0; u < NL; ++u) {
-          const int idx = base + u * kBlock + threadIdx.x;
-          const int c = idx / per, r = idx - c * per;
-          const int cil = r / tp;
-          const bool ok = idx < R * per && co0 + c < d.Co && ci0 + cil < d.Ci;
-          v[u] = ok ? d.w[((int64_t)(co0 + c) * d.Ci + ci0) * tp + r] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-          const int idx = base + u * kBlock + threadIdx.x;
-          const int c = idx / per, r = idx - c * per;
-          const int cil = r / tp, tap = r - cil * tp;
-          if (idx < R * per) ptile[(c * tp + tap) * kPackRow + cil] = v[u];
-        }
-      }
-      __syncthreads();
-      for (int idx = threadIdx.x; idx < R * tp * 8; idx += kBlock) {
-        const int row = idx >> 3, cil = (idx & 7) * 8;
-        const int c = row / tp, tap = row - c * tp;
-        if (co0 + c < d.Co && ci0 + cil < d.Cip) {
-          float f[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = ptile[row * kPackRow + cil + k];
-          store8(out + ((int64_t)(co0 + c) * tp + tap) * d.Cip + ci0 + cil, f);
-        }
-      }
-    } else {  // out[ci][tap][co], tile R ci x 64 co
-      constexpr int R = pack_rows(TAPS ? TAPS : kPackMaxTaps, true);
-      const int nob = (d.Cop + 63) / 64;
-      const int ci0 = (lt / nob) * R, co0 = (lt % nob) * 64;
-      const int per = R * tp;
-      constexpr int NL = TAPS ? (64 * R * TAPS + kBlock - 1) / kBlock : 1;
-      for (int base = 0; base < 64 * per; base += NL * kBlock) {
-        float v[NL];
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-          const int idx = base + u * kBlock + threadIdx.x;
-          const int col = idx / per, r = idx - col * per;
-          const int cil = r / tp;
-          const bool ok = idx < 64 * per && co0 + col < d.Co && ci0 + cil < d.Ci;
-          v[u] = ok ? d.w[((int64_t)(co0 + col) * d.Ci + ci0) * tp + r] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-          const int idx = base + u * kBlock + threadIdx.x;
-          const int col = idx / per, r = idx - col * per;
-          const int cil = r / tp, tap = r - cil * tp;
-          if (idx < 64 * per) ptile[(cil * tp + tap) * kPackRow + col] = v[u];
-        }
-      }
-      __syncthreads();
-      for (int idx = threadIdx.x; idx < R * tp * 8; idx += kBlock) {
-        const int row = idx >> 3, col = (idx & 7) * 8;
-        const int cil = row / tp, tap = row - cil * tp;
-        if (ci0 + cil < d.Cip && co0 + col < d.Cop) {
-          float f[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = ptile[row * kPackRow + col + k];
-          store8(out + ((int64_t)(ci0 + cil) * tp + tap) * d.Cop + co0 + col, f);
-        }
-      }
+    for (int u = 0; u < NL; ++u) {
+      const int idx = base + u * kBlock + threadIdx.x;
+      const int row = idx / per, r = idx - row * per;    // row: co offset (both layouts read
+      const int cil = r / tp, tap = r - cil * tp;        // w[co] rows); r: (ci offset, tap)
+      const bool ok = idx < nrows * per && row < co_lim && cil < ci_lim;
+      v[u] = ok ? src[row * rowlen + r] : 0.f;
+      // LDS [outer][tap][inner]: non-transposed outer = co (row), inner = ci (cil);
+      // transposed outer = ci (cil), inner = co (row)
+      dst[u] = idx < nrows * per ? ((tr ? cil : row) * tp + tap) * kPackRow + (tr ? row : cil)
+                                 : -1;
     }
+#pragma unroll
+    for (int u = 0; u < NL; ++u)
+      if (dst[u] >= 0) ptile[dst[u]] = v[u];
+  }
+  __syncthreads();
+  const int orows = tr ? RT : RN;                        // output rows: (outer, tap)
+  const int olim = tr ? d.Cip - ci0 : d.Co - co0;
+  T* out = (T*)d.out;
+  for (int idx = threadIdx.x; idx < orows * tp * 8; idx += kBlock) {
+    const int row = idx >> 3, c8 = (idx & 7) * 8;
+    const int o = row / tp, tap = row - o * tp;
+    if (o < olim && inner0 + c8 < ninner) {
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = ptile[row * kPackRow + c8 + k];
+      store8(out + ((int64_t)(outer0 + o) * tp + tap) * ninner + inner0 + c8, f);
+    }
+  }
 }
 
 template <typename T>
