@@ -1185,14 +1185,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_wide_kernel(WgtGeom g, int wc,
 // transposed fragments instead of 16 KiB: the COT = 64 form needs 128 B/clk of LDS per CU at
 // the MFMA rate (two workgroups per CU), the LDS peak, and is LDS-bound; this one needs 64.
 // The waves' partial tiles are added through LDS after the loop, in wave order (fixed).
-// SHIFT (round 5): the kw taps 1 and 2 of a B fragment are tap 0's eight strip pixels shifted
-// by one / two positions plus the next one / two -- v_alignbit on the register pairs and one
-// 2-byte LDS read per extra pixel, instead of two ds_read_b64_tr_b16 per fragment and tap.
-// The eight pixels of a lane's fragment lie in one strip row (64 % wc == 0, wc % 8 == 0), and
-// s + 8, s + 9 are still in it (the strip row's two halo columns), so the shifted values are
-// exactly the tap's own reads: bit-identical results.
-template <int RW, int COT, int NST, bool ONE, bool PLANE = false, bool KS = false,
-          bool SHIFT = false>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
+template <int RW, int COT, int NST, bool ONE, bool PLANE = false, bool KS = false>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
 __global__ __launch_bounds__(kThreads, (PLANE || KS) ? 1 : 2) void wgrad_dma_kernel(
     WgtGeom g, int wc, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
     float* __restrict__ dw) {
@@ -1360,32 +1353,12 @@ __global__ __launch_bounds__(kThreads, (PLANE || KS) ? 1 : 2) void wgrad_dma_ker
       }
       const int s_lo = ONE ? p_lo : (p_lo / wc) * SW + p_lo % wc;
       const int s_hi = ONE ? p_hi : (p_hi / wc) * SW + p_hi % wc;
-      constexpr bool SH = SHIFT && !ONE && !PLANE && NT == 3;
-      uint32_t ext[2][2] = {{0u, 0u}, {0u, 0u}};  // SH: strip pixels s + 8, s + 9 per j
-      if constexpr (SH) {
-        const int s_b = s_lo - q4;  // strip position of the lane's first fragment pixel
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int ci = wn * 32 + 16 * j + fr;
-          ext[j][0] = Xs[wg_off(s_b + 8, ci)];
-          ext[j][1] = Xs[wg_off(s_b + 9, ci)];
-        }
-      }
-      bf16x8 bfr[2];
 #pragma unroll
       for (int tc = 0; tc < NT; ++tc) {
+        bf16x8 bfr[2];
         const int sh_t = PLANE ? (tc / 3) * SW + tc % 3 : tc;  // strip shift of the tap
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          if (SH && tc > 0) {  // tap tc = tap tc-1 shifted by one strip pixel
-            uint4 u = __builtin_bit_cast(uint4, bfr[j]);
-            u = make_uint4(__builtin_amdgcn_alignbit(u.y, u.x, 16),
-                           __builtin_amdgcn_alignbit(u.z, u.y, 16),
-                           __builtin_amdgcn_alignbit(u.w, u.z, 16),
-                           __builtin_amdgcn_alignbit(ext[j][tc - 1], u.w, 16));
-            bfr[j] = __builtin_bit_cast(bf16x8, u);
-            continue;
-          }
           const int c = wn * 32 + 16 * j + 4 * p4;
           const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (lds_bf16x4*)(Xs + wg_off(s_lo + sh_t, c)));
@@ -2412,10 +2385,6 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     if (dry) return VD_OK;
     dim3 grid((unsigned)tiles, (unsigned)splits);
     // XCD-aware 1-D grid (A/B knob VDIFF_WGRAD_XCD=0 restores the 2-D grid)
-    static const int g_wgrad_shift = [] {  // tap-shifted B fragments (SHIFT); 0: A/B
-      const char* e = getenv("VDIFF_WGRAD_SHIFT");
-      return e ? atoi(e) : 1;
-    }();
     static const int wxcd = [] {
       const char* e = getenv("VDIFF_WGRAD_XCD");
       return e ? atoi(e) : 1;
@@ -2463,25 +2432,18 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     else if (one && w1_nst >= 4) VD_WGD(64, 64, 4, true);
     else if (one) VD_WGD(64, 64, 2, true);
     else if (plane) VD_WGD(224, 64, 2, false, true);
-    // kw-strip kernels: tap-shifted B fragments (SHIFT) unless VDIFF_WGRAD_SHIFT=0 (A/B)
-#define VD_WGD3(RW, COT, NST)                                                              \
-  do {                                                                                     \
-    if (g_wgrad_shift) VD_WGD(RW, COT, NST, false, false, false, true);                     \
-    else VD_WGD(RW, COT, NST, false);                                                      \
-  } while (0)
-    else if (cot == 128 && w3_nst >= 3 && rows <= 96) VD_WGD3(96, 128, 3);
-    else if (cot == 128 && w3_nst >= 3 && rows <= 128) VD_WGD3(128, 128, 3);
-    else if (cot == 128 && w3_nst >= 3) VD_WGD3(192, 128, 3);
-    else if (cot == 128 && rows <= 96) VD_WGD3(96, 128, 2);
-    else if (cot == 128 && rows <= 128) VD_WGD3(128, 128, 2);
-    else if (cot == 128) VD_WGD3(192, 128, 2);
-    else if (w3_nst >= 3 && rows <= 96) VD_WGD3(96, 64, 3);
-    else if (w3_nst >= 3 && rows <= 128) VD_WGD3(128, 64, 3);
-    else if (w3_nst >= 3) VD_WGD3(192, 64, 3);
-    else if (rows <= 96) VD_WGD3(96, 64, 2);
-    else if (rows <= 128) VD_WGD3(128, 64, 2);
-    else VD_WGD3(192, 64, 2);
-#undef VD_WGD3
+    else if (cot == 128 && w3_nst >= 3 && rows <= 96) VD_WGD(96, 128, 3, false);
+    else if (cot == 128 && w3_nst >= 3 && rows <= 128) VD_WGD(128, 128, 3, false);
+    else if (cot == 128 && w3_nst >= 3) VD_WGD(192, 128, 3, false);
+    else if (cot == 128 && rows <= 96) VD_WGD(96, 128, 2, false);
+    else if (cot == 128 && rows <= 128) VD_WGD(128, 128, 2, false);
+    else if (cot == 128) VD_WGD(192, 128, 2, false);
+    else if (w3_nst >= 3 && rows <= 96) VD_WGD(96, 64, 3, false);
+    else if (w3_nst >= 3 && rows <= 128) VD_WGD(128, 64, 3, false);
+    else if (w3_nst >= 3) VD_WGD(192, 64, 3, false);
+    else if (rows <= 96) VD_WGD(96, 64, 2, false);
+    else if (rows <= 128) VD_WGD(128, 64, 2, false);
+    else VD_WGD(192, 64, 2, false);
 #undef VD_WGD
     return vd::check_launch("conv_wgrad_dma");
   }

@@ -238,42 +238,3 @@ def test_conv_wgrad_round4_split_rule(shape, Co, k):
     assert torch.equal(a, b)
     ref = _wgrad(ops.to_cl(x.float()), w, ops.to_cl(dy.float()), 1, pad, False)
     assert rel_l2(a, ref) < 1e-5, rel_l2(a, ref)
-
-
-_SHIFT_CASES = [((1, 64, 16, 128, 128), 64), ((1, 256, 16, 32, 32), 256), ((1, 128, 4, 16, 16), 64),
-                ((2, 200, 4, 64, 64), 64), ((1, 384, 16, 64, 64), 128)]
-
-
-def _shift_case_grads():
-    from vdiff import ops
-    out = []
-    for i, (shape, Co) in enumerate(_SHIFT_CASES):
-        x = ops.to_cl(seeded(shape, 40 + i).to(dev, torch.bfloat16))
-        w = (seeded((Co, shape[1], 3, 3, 3), 50 + i) / (shape[1] * 27) ** 0.5).to(dev)
-        y = ops.conv(x, w, None, padding=1)
-        dy = ops.to_cl(seeded(tuple(y.shape), 60 + i).to(dev, torch.bfloat16))
-        out.append(_wgrad(x, w, dy, 1, 1, False).cpu())
-    return out
-
-
-def test_conv_wgrad_tap_shift_bit_identical(tmp_path):
-    """Round 5: the kw-strip weight gradient builds the kw taps 1 / 2 of each B fragment by
-    shifting tap 0's eight strip pixels (v_alignbit + one 2-byte LDS read per extra pixel)
-    instead of re-reading them transposed -- the same bf16 operands in the same MFMA order, so
-    the gradient must equal the re-reading kernel's (VDIFF_WGRAD_SHIFT=0, read once per
-    process: run in a child process) bit for bit, at widths 128 / 64 / 32 / 16 and padded Ci."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    f = tmp_path / "noshift.pt"
-    code = ("import sys, torch; sys.path[:0] = [%r, %r, %r]; import conftest; "
-            "import test_gpu_conv as t; torch.save(t._shift_case_grads(), %r)"
-            % (here, os.path.join(os.path.dirname(here), "lipreading-video-generation_amd"),
-               os.path.dirname(here), str(f)))
-    env = dict(os.environ, VDIFF_WGRAD_SHIFT="0")
-    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300)
-    ref = torch.load(str(f), weights_only=True)
-    got = _shift_case_grads()
-    for (shape, Co), a, b in zip(_SHIFT_CASES, got, ref):
-        assert torch.equal(a, b), (shape, Co, rel_l2(a, b))
