@@ -15,7 +15,8 @@ T*H*W tokens (the reference semantics), bf16 activations / fp32 master weights,
 dropout 0.1 in train mode, random-init wav2vec2-base audio encoder (trainable, as
 the reference), Adam at --lr (default 1e-3; train.py:102 uses 1e-2, at which this init
 diverges within 25 steps -- DESIGN section 5).  One synthetic clip [1, 3, 16, 128, 128] (+16 audio
-windows of 4000 samples) per GPU, resident in HBM before timing.  A step = q_sample
+windows of 4000 samples) per GPU and step -- a bank of distinct clips with their own noise and
+timestep, generated on the device before timing (train.py:122-125 draws new ones each step).  A step = q_sample
 + forward + MSE + backward + RCCL gradient all-reduce + Adam.  Weak scaling.
 
 Secondary: DDIM steps/sec = one 50-step-DDIM denoising step (UNet forward at
@@ -142,6 +143,16 @@ def build_model(args, device, audio_attention=False, init=None):
     if (init or getattr(args, "init", "nonzero")) == "nonzero":
         reinit_nonzero(model, seed=1234)
     return model.to(device)
+
+
+def clip_bank(args, n, device, seed):
+    """n distinct synthetic train clips (x0, cond, audio, eps, t), generated on the device
+    before the timed region (resident in HBM): each step trains on its own clip with its own
+    noise and timestep, as the reference loop draws a new batch, torch.randn_like(im) and
+    randint t every step (train.py:122-125)."""
+    from vdiff.engine import synthetic_clip
+    return [synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device,
+                           seed=seed * 1000 + i) for i in range(n)]
 
 
 def ddim_stepper(args, model, sampler, cond, feats, xt):
@@ -405,15 +416,15 @@ def xattn_leg(args, rank, world, device, base_ms):
     broadcast_parameters(model)
     work = unet_forward_work(model, (args.clips_per_gpu, 195, args.frames, args.size, args.size))
     tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=args.lr)
-    clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
     nsteps = args.steps if args.xattn_steps < 0 else args.xattn_steps
+    bank = clip_bank(args, args.warmup + nsteps, device, rank)
     losses = []
-    for _ in range(args.warmup):
-        losses.append(tr.step(clip))
+    for i in range(args.warmup):
+        losses.append(tr.step(bank[i]))
     barrier_sync(world)
     t0 = time.perf_counter()
-    for _ in range(nsteps):
-        losses.append(tr.step(clip))
+    for i in range(nsteps):
+        losses.append(tr.step(bank[args.warmup + i]))
     barrier_sync(world)
     el = max_over_ranks(time.perf_counter() - t0, world, device)
     ms = el / nsteps * 1e3
@@ -480,15 +491,15 @@ def st_leg(args, rank, world, device):
     broadcast_parameters(model)
     work = unet_forward_work(model, (args.clips_per_gpu, 195, args.frames, args.size, args.size))
     tr = Trainer(model, LinearNoiseScheduler(100, 0.00085, 0.012), lr=args.lr)
-    clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
     nsteps = args.steps if args.st_steps < 0 else args.st_steps
-    losses = [tr.step(clip) for _ in range(args.warmup)]
+    bank = clip_bank(args, args.warmup + nsteps, device, rank)
+    losses = [tr.step(bank[i]) for i in range(args.warmup)]
     barrier_sync(world)
     timer = ops.KernelTimer(attention=True, convs=False)
     ops.set_timer(timer)
     t0 = time.perf_counter()
-    for _ in range(nsteps):
-        losses.append(tr.step(clip))
+    for i in range(nsteps):
+        losses.append(tr.step(bank[args.warmup + i]))
     barrier_sync(world)
     el = time.perf_counter() - t0
     ops.set_timer(None)
@@ -662,9 +673,9 @@ def main():
     train_losses = []
     if args.only in ("train", "all"):
         trainer = Trainer(model, sched, lr=args.lr)
-        clip = synthetic_clip(args.clips_per_gpu, args.frames, args.size, 100, device, seed=rank)
+        bank = clip_bank(args, args.warmup + args.steps, device, rank)
         for i in range(args.warmup):
-            loss = trainer.step(clip)
+            loss = trainer.step(bank[i])
             train_losses.append(loss)
             log(f"warmup {i}: loss {float(loss):.4f}")
         barrier_sync(world)
@@ -675,8 +686,8 @@ def main():
         if trainer.bucketer is not None:
             trainer.bucketer.timing = True
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            loss = trainer.step(clip)
+        for i in range(args.steps):
+            loss = trainer.step(bank[args.warmup + i])
             train_losses.append(loss)  # device scalars: read after the timed region
         barrier_sync(world)
         el = time.perf_counter() - t0
@@ -708,7 +719,7 @@ def main():
             log("  kernel", r)
         ctimer = ops.KernelTimer(attention=False, convs=True)
         ops.set_timer(ctimer)
-        trainer.step(clip)  # untimed: per-launch conv times
+        trainer.step(bank[-1])  # untimed: per-launch conv times
         ops.set_timer(None)
         conv = ctimer.conv_summary()
         by_kind = {}
@@ -725,7 +736,7 @@ def main():
         for (kind, key), (cnt, tot, flop) in sorted(conv.items(), key=lambda kv: -kv[1][1])[:60]:
             log(f"  conv {kind:16s} {key:40s} x{cnt:<3d} {tot:7.2f} ms/step "
                 f"{flop * cnt / (tot / 1e3) / 1e12:7.1f} TF/s")
-        del trainer
+        del trainer, bank
         torch.cuda.empty_cache()
 
     if args.only in ("ddim", "all"):
