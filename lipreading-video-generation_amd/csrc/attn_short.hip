@@ -22,6 +22,7 @@
 // qkv buffer.  No barrier: each wave has its own LDS region.
 #include "vd_common.h"
 #include <math.h>
+#include <cstdlib>
 
 namespace {
 
@@ -98,23 +99,38 @@ __device__ __forceinline__ void lds_fence() {
 }
 
 // ---------------------------------------------------------------- forward
-template <int D, int NB, int WPB>
-__global__ void __launch_bounds__(64 * WPB) short_attn_fwd_kernel(ShortArgs a) {
-  constexpr int KS = D / 32, DB = D / 16, Lp = 16 * NB;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[WPB * Lp * kRowS<D>];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // every lane of the wave stays in (the transposed read needs EXEC all ones): a wave past
-  // the last sequence reads sequence nseq - 1 and stores nothing
-  const int s_raw = blockIdx.x * WPB + w;
-  const bool live = s_raw < a.nseq;
-  const int s = live ? s_raw : a.nseq - 1;
-  const int L = a.seq_len, col = lane & 15, grp = lane >> 4;
-  bf16_t* vt = lds + w * Lp * kRowS<D>;
-  const int64_t base = seq_off(s, a.groups, a.bs, a.gs);
-  const bf16_t* qp = a.q + base;
-  const bf16_t* kp = a.k + base;
-  const bf16_t* vp = a.v + base;
+// SPW sequences per wave, one after the other, with the next sequence's q / k / v fragments
+// loaded before the current one is computed (its HBM latency under this one's MFMAs and
+// softmax); the waves of a workgroup take neighbouring pixels at each of their SPW steps, so
+// a workgroup streams WPB * SPW adjacent token rows per frame.
+template <int D, int NB>
+struct FwdFrags {
+  static constexpr int KS = D / 32;
+  bf16x8 q[KS][NB], k[KS][NB], v[KS][NB];
+};
 
+template <int D, int NB>
+__device__ __forceinline__ void fwd_load(const ShortArgs& a, int s, FwdFrags<D, NB>& f, int col,
+                                         int grp) {
+  const int64_t base = seq_off(s, a.groups, a.bs, a.gs);
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int r = 16 * b + col, c = ks * 32 + 8 * grp;
+      const bool ok = r < a.seq_len;
+      const int64_t off = base + (int64_t)r * a.ts + c;
+      f.q[ks][b] = ld16(a.q + off, ok);
+      f.k[ks][b] = ld16(a.k + off, ok);
+      f.v[ks][b] = ld16(a.v + off, ok);
+    }
+}
+
+template <int D, int NB>
+__device__ __forceinline__ void fwd_one(const ShortArgs& a, int s, bool live,
+                                        const FwdFrags<D, NB>& f, bf16_t* vt, int lane) {
+  constexpr int KS = D / 32, DB = D / 16;
+  const int L = a.seq_len, col = lane & 15, grp = lane >> 4;
   f32x4 st[NB][NB];  // S^T[kb][qb]: column = query, rows = keys
 #pragma unroll
   for (int i = 0; i < NB; ++i)
@@ -122,21 +138,14 @@ __global__ void __launch_bounds__(64 * WPB) short_attn_fwd_kernel(ShortArgs a) {
     for (int j = 0; j < NB; ++j) st[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    const int c = ks * 32 + 8 * grp;
-    bf16x8 qf[NB], kf[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int r = 16 * b + col;
-      const bool ok = r < L;
-      qf[b] = ld16(qp + (int64_t)r * a.ts + c, ok);
-      kf[b] = ld16(kp + (int64_t)r * a.ts + c, ok);
-      st_frag<D>(vt, r, c, ld16(vp + (int64_t)r * a.ts + c, ok));
-    }
+    for (int b = 0; b < NB; ++b) st_frag<D>(vt, 16 * b + col, ks * 32 + 8 * grp, f.v[ks][b]);
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
       for (int qb = 0; qb < NB; ++qb)
-        st[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kb], qf[qb], st[kb][qb], 0, 0, 0);
+        st[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k[ks][kb], f.q[ks][qb],
+                                                             st[kb][qb], 0, 0, 0);
   }
   const float c2 = a.scale * kLog2eS;
   bf16x4 pb[NB][NB];
@@ -191,6 +200,30 @@ __global__ void __launch_bounds__(64 * WPB) short_attn_fwd_kernel(ShortArgs a) {
             make_uint2(lo, hi);
       }
     }
+  }
+}
+
+template <int D, int NB, int WPB, int SPW>
+__global__ void __launch_bounds__(64 * WPB) short_attn_fwd_kernel(ShortArgs a) {
+  constexpr int Lp = 16 * NB;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[WPB * Lp * kRowS<D>];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  bf16_t* vt = lds + w * Lp * kRowS<D>;
+  // every lane of the wave stays in (the transposed read needs EXEC all ones): a step past
+  // the last sequence reads sequence nseq - 1 and stores nothing
+  const int s0 = blockIdx.x * WPB * SPW + w;
+  FwdFrags<D, NB> cur, nxt;
+  fwd_load<D, NB>(a, s0 < a.nseq ? s0 : a.nseq - 1, cur, col, grp);
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) {
+    const int s = s0 + i * WPB;
+    if (i + 1 < SPW) {
+      const int sn = s + WPB;
+      fwd_load<D, NB>(a, sn < a.nseq ? sn : a.nseq - 1, nxt, col, grp);
+    }
+    fwd_one<D, NB>(a, s < a.nseq ? s : a.nseq - 1, s < a.nseq, cur, vt, lane);
+    if (i + 1 < SPW) cur = nxt;
   }
 }
 
@@ -341,10 +374,23 @@ constexpr int wpb() {
   return 4 * per_wave <= 65536 ? 4 : 2 * per_wave <= 65536 ? 2 : 1;
 }
 
+// sequences per wave in the forward: 2 (prefetching the second) where the two fragment sets
+// fit (D * NB <= 128: 48 VGPRs of fragments at D = 64), else 1
+int g_short_spw = [] {
+  const char* e = std::getenv("VDIFF_SHORT_SPW");
+  return e ? std::atoi(e) : 2;
+}();
+
 template <int D, int NB>
 int launch_fwd(const ShortArgs& a, hipStream_t st) {
   constexpr int W = wpb<D, NB, 1>();
-  short_attn_fwd_kernel<D, NB, W><<<(a.nseq + W - 1) / W, 64 * W, 0, st>>>(a);
+  if (D * NB <= 128 && g_short_spw >= 4) {
+    short_attn_fwd_kernel<D, NB, W, 4><<<(a.nseq + 4 * W - 1) / (4 * W), 64 * W, 0, st>>>(a);
+  } else if (D * NB <= 128 && g_short_spw >= 2) {
+    short_attn_fwd_kernel<D, NB, W, 2><<<(a.nseq + 2 * W - 1) / (2 * W), 64 * W, 0, st>>>(a);
+  } else {
+    short_attn_fwd_kernel<D, NB, W, 1><<<(a.nseq + W - 1) / W, 64 * W, 0, st>>>(a);
+  }
   return vd::check_launch("short_attn_fwd");
 }
 template <int D, int NB>
