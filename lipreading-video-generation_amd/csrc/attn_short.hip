@@ -180,7 +180,10 @@ __device__ __forceinline__ void fwd_one(const ShortArgs& a, int s, bool live,
     if (live && grp == 0 && qr < L) a.lse[(int64_t)s * L + qr] = (m + log2f(l)) / kLog2eS;
   }
   lds_fence();
-  bf16_t* op = a.out + seq_off(s, a.groups, a.obs, a.ogs);
+  // O^T (column = query, rows = d 16 db + 4 grp + i) into the wave's [Lp][D + 8] O image,
+  // then written out as whole rows: 16 B per lane, a row's D * 2 bytes by consecutive lanes
+  // (8-B stores of 4 d each had every lane-group write a quarter of a cache line)
+  bf16_t* ot = vt + 16 * NB * kRowS<D>;
 #pragma unroll
   for (int db = 0; db < DB; ++db) {
     bf16x4 vtr[NB];
@@ -192,24 +195,31 @@ __device__ __forceinline__ void fwd_one(const ShortArgs& a, int s, bool live,
 #pragma unroll
       for (int kb = 0; kb < NB; ++kb)
         acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vtr[kb], pb[kb][qb], acc, 0, 0, 0);
-      const int qr = 16 * qb + col;  // O^T: column = query, rows = d 16 db + 4 grp + i
-      if (live && qr < L) {
-        const uint32_t lo = pack2bf(acc[0] * rl[qb], acc[1] * rl[qb]);
-        const uint32_t hi = pack2bf(acc[2] * rl[qb], acc[3] * rl[qb]);
-        *reinterpret_cast<uint2*>(op + (int64_t)qr * a.ots + 16 * db + 4 * grp) =
-            make_uint2(lo, hi);
-      }
+      const uint32_t lo = pack2bf(acc[0] * rl[qb], acc[1] * rl[qb]);
+      const uint32_t hi = pack2bf(acc[2] * rl[qb], acc[3] * rl[qb]);
+      *reinterpret_cast<uint2*>(ot + (16 * qb + col) * kRowS<D> + 16 * db + 4 * grp) =
+          make_uint2(lo, hi);
     }
+  }
+  lds_fence();
+  bf16_t* op = a.out + seq_off(s, a.groups, a.obs, a.ogs);
+  constexpr int CPR = D / 8;                      // 16-B chunks per row
+#pragma unroll
+  for (int k = 0; k < (16 * NB * CPR + 63) / 64; ++k) {
+    const int idx = k * 64 + lane, r = idx / CPR, c = (idx % CPR) * 8;
+    if (live && r < L && idx < 16 * NB * CPR)
+      *reinterpret_cast<bf16x8*>(op + (int64_t)r * a.ots + c) =
+          *reinterpret_cast<const bf16x8*>(ot + r * kRowS<D> + c);
   }
 }
 
 template <int D, int NB, int WPB, int SPW>
 __global__ void __launch_bounds__(64 * WPB) short_attn_fwd_kernel(ShortArgs a) {
   constexpr int Lp = 16 * NB;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[WPB * Lp * kRowS<D>];
+  __shared__ __attribute__((aligned(16))) bf16_t lds[WPB * 2 * Lp * kRowS<D>];  // V | O images
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
-  bf16_t* vt = lds + w * Lp * kRowS<D>;
+  bf16_t* vt = lds + w * 2 * Lp * kRowS<D>;
   // every lane of the wave stays in (the transposed read needs EXEC all ones): a step past
   // the last sequence reads sequence nseq - 1 and stores nothing
   const int s0 = blockIdx.x * WPB * SPW + w;
@@ -383,7 +393,7 @@ int g_short_spw = [] {
 
 template <int D, int NB>
 int launch_fwd(const ShortArgs& a, hipStream_t st) {
-  constexpr int W = wpb<D, NB, 1>();
+  constexpr int W = wpb<D, NB, 2>();  // V and O images
   if (D * NB <= 128 && g_short_spw >= 4) {
     short_attn_fwd_kernel<D, NB, W, 4><<<(a.nseq + 4 * W - 1) / (4 * W), 64 * W, 0, st>>>(a);
   } else if (D * NB <= 128 && g_short_spw >= 2) {
