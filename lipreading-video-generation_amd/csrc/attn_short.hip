@@ -99,10 +99,11 @@ __device__ __forceinline__ void lds_fence() {
 }
 
 // ---------------------------------------------------------------- forward
-// SPW sequences per wave, one after the other, with the next sequence's q / k / v fragments
-// loaded before the current one is computed (its HBM latency under this one's MFMAs and
-// softmax); the waves of a workgroup take neighbouring pixels at each of their SPW steps, so
-// a workgroup streams WPB * SPW adjacent token rows per frame.
+// One wave per sequence: q / k / v fragments straight from HBM into registers (16 B per
+// lane), S^T on 16x16 MFMA tiles with the query on the lane column, the softmax in registers,
+// V^T through the wave's LDS image by transposed reads, O staged through a second image and
+// written as whole rows.  (Two or four sequences per wave with the next one's fragments
+// prefetched measured the same: the kernel is store / occupancy bound, not load-latency bound.)
 template <int D, int NB>
 struct FwdFrags {
   static constexpr int KS = D / 32;
@@ -213,28 +214,20 @@ __device__ __forceinline__ void fwd_one(const ShortArgs& a, int s, bool live,
   }
 }
 
-template <int D, int NB, int WPB, int SPW>
+template <int D, int NB, int WPB>
 __global__ void __launch_bounds__(64 * WPB) short_attn_fwd_kernel(ShortArgs a) {
   constexpr int Lp = 16 * NB;
   __shared__ __attribute__((aligned(16))) bf16_t lds[WPB * 2 * Lp * kRowS<D>];  // V | O images
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
   bf16_t* vt = lds + w * 2 * Lp * kRowS<D>;
-  // every lane of the wave stays in (the transposed read needs EXEC all ones): a step past
+  // every lane of the wave stays in (the transposed read needs EXEC all ones): a wave past
   // the last sequence reads sequence nseq - 1 and stores nothing
-  const int s0 = blockIdx.x * WPB * SPW + w;
-  FwdFrags<D, NB> cur, nxt;
-  fwd_load<D, NB>(a, s0 < a.nseq ? s0 : a.nseq - 1, cur, col, grp);
-#pragma unroll
-  for (int i = 0; i < SPW; ++i) {
-    const int s = s0 + i * WPB;
-    if (i + 1 < SPW) {
-      const int sn = s + WPB;
-      fwd_load<D, NB>(a, sn < a.nseq ? sn : a.nseq - 1, nxt, col, grp);
-    }
-    fwd_one<D, NB>(a, s < a.nseq ? s : a.nseq - 1, s < a.nseq, cur, vt, lane);
-    if (i + 1 < SPW) cur = nxt;
-  }
+  const int s = blockIdx.x * WPB + w;
+  const int sc = s < a.nseq ? s : a.nseq - 1;
+  FwdFrags<D, NB> f;
+  fwd_load<D, NB>(a, sc, f, col, grp);
+  fwd_one<D, NB>(a, sc, s < a.nseq, f, vt, lane);
 }
 
 // ---------------------------------------------------------------- backward (fused)
@@ -338,6 +331,11 @@ __global__ void __launch_bounds__(64 * WPB) short_attn_bwd_kernel(ShortArgs a) {
   bf16_t* dqp = a.out + base;
   bf16_t* dkp = a.dk + base;
   bf16_t* dvp = a.dv + base;
+  // STAGE: the packed outputs are kept in registers and, once every transposed read is done,
+  // written through the Q / K / dO images as whole rows (16 B per lane; 8-B stores of 4 d
+  // each write a quarter of a cache line per lane group).  Larger D * NB stores directly.
+  constexpr bool STAGE = 3 * DB * NB * 2 <= 96;
+  uint2 outq[STAGE ? DB : 1][NB], outk[STAGE ? DB : 1][NB], outv[STAGE ? DB : 1][NB];
 #pragma unroll
   for (int db = 0; db < DB; ++db) {
     bf16x4 qtr[NB], ktr[NB], dtr[NB];
@@ -359,17 +357,50 @@ __global__ void __launch_bounds__(64 * WPB) short_attn_bwd_kernel(ShortArgs a) {
         ak = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(qtr[j], dsy[j][b], ak, 0, 0, 0);
         av = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(dtr[j], pyb[j][b], av, 0, 0, 0);
       }
-      const int r = 16 * b + col;
-      if (live && r < L) {
-        const int64_t off = (int64_t)r * a.ts + 16 * db + 4 * grp;
-        *reinterpret_cast<uint2*>(dqp + off) =
-            make_uint2(pack2bf(aq[0] * a.scale, aq[1] * a.scale),
-                       pack2bf(aq[2] * a.scale, aq[3] * a.scale));
-        *reinterpret_cast<uint2*>(dkp + off) =
-            make_uint2(pack2bf(ak[0] * a.scale, ak[1] * a.scale),
-                       pack2bf(ak[2] * a.scale, ak[3] * a.scale));
-        *reinterpret_cast<uint2*>(dvp + off) = make_uint2(pack2bf(av[0], av[1]),
-                                                          pack2bf(av[2], av[3]));
+      const uint2 vq = make_uint2(pack2bf(aq[0] * a.scale, aq[1] * a.scale),
+                                  pack2bf(aq[2] * a.scale, aq[3] * a.scale));
+      const uint2 vk = make_uint2(pack2bf(ak[0] * a.scale, ak[1] * a.scale),
+                                  pack2bf(ak[2] * a.scale, ak[3] * a.scale));
+      const uint2 vv = make_uint2(pack2bf(av[0], av[1]), pack2bf(av[2], av[3]));
+      if constexpr (STAGE) {
+        outq[db][b] = vq;
+        outk[db][b] = vk;
+        outv[db][b] = vv;
+      } else {
+        const int r = 16 * b + col;
+        if (live && r < L) {
+          const int64_t off = (int64_t)r * a.ts + 16 * db + 4 * grp;
+          *reinterpret_cast<uint2*>(dqp + off) = vq;
+          *reinterpret_cast<uint2*>(dkp + off) = vk;
+          *reinterpret_cast<uint2*>(dvp + off) = vv;
+        }
+      }
+    }
+  }
+  if constexpr (STAGE) {
+    lds_fence();  // every transposed read of the images has returned
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int o = (16 * b + col) * kRowS<D> + 16 * db + 4 * grp;
+        *reinterpret_cast<uint2*>(qt + o) = outq[db][b];
+        *reinterpret_cast<uint2*>(kt + o) = outk[db][b];
+        *reinterpret_cast<uint2*>(dt + o) = outv[db][b];
+      }
+    lds_fence();
+    constexpr int CPR = D / 8;  // 16-B chunks per row
+#pragma unroll
+    for (int k = 0; k < (16 * NB * CPR + 63) / 64; ++k) {
+      const int idx = k * 64 + lane, r = idx / CPR, c = (idx % CPR) * 8;
+      if (live && r < L && idx < 16 * NB * CPR) {
+        const int64_t off = (int64_t)r * a.ts + c;
+        *reinterpret_cast<bf16x8*>(dqp + off) =
+            *reinterpret_cast<const bf16x8*>(qt + r * kRowS<D> + c);
+        *reinterpret_cast<bf16x8*>(dkp + off) =
+            *reinterpret_cast<const bf16x8*>(kt + r * kRowS<D> + c);
+        *reinterpret_cast<bf16x8*>(dvp + off) =
+            *reinterpret_cast<const bf16x8*>(dt + r * kRowS<D> + c);
       }
     }
   }
@@ -384,23 +415,10 @@ constexpr int wpb() {
   return 4 * per_wave <= 65536 ? 4 : 2 * per_wave <= 65536 ? 2 : 1;
 }
 
-// sequences per wave in the forward: 2 (prefetching the second) where the two fragment sets
-// fit (D * NB <= 128: 48 VGPRs of fragments at D = 64), else 1
-int g_short_spw = [] {
-  const char* e = std::getenv("VDIFF_SHORT_SPW");
-  return e ? std::atoi(e) : 2;
-}();
-
 template <int D, int NB>
 int launch_fwd(const ShortArgs& a, hipStream_t st) {
   constexpr int W = wpb<D, NB, 2>();  // V and O images
-  if (D * NB <= 128 && g_short_spw >= 4) {
-    short_attn_fwd_kernel<D, NB, W, 4><<<(a.nseq + 4 * W - 1) / (4 * W), 64 * W, 0, st>>>(a);
-  } else if (D * NB <= 128 && g_short_spw >= 2) {
-    short_attn_fwd_kernel<D, NB, W, 2><<<(a.nseq + 2 * W - 1) / (2 * W), 64 * W, 0, st>>>(a);
-  } else {
-    short_attn_fwd_kernel<D, NB, W, 1><<<(a.nseq + W - 1) / W, 64 * W, 0, st>>>(a);
-  }
+  short_attn_fwd_kernel<D, NB, W><<<(a.nseq + W - 1) / W, 64 * W, 0, st>>>(a);
   return vd::check_launch("short_attn_fwd");
 }
 template <int D, int NB>
