@@ -480,10 +480,17 @@ def gen_dq(probe=None):
 
 def main():
     out = sys.argv[1]
-    for arg in sys.argv[2:]:  # A/B code-placement builds only (tools/build_asm_phase.sh)
+    for arg in sys.argv[2:]:  # A/B builds only (tools/build_asm_phase.sh, build_asm_knobs.sh)
         if arg.startswith("--phase="):
             import asmgen
             asmgen.PHASE_FLIP = arg[len("--phase="):]
+        elif arg.startswith("--knob="):  # --knob=module.NAME=int, e.g. gen_fwd.CHAINS=4
+            import importlib
+            target, val = arg[len("--knob="):].split("=")
+            mod, name = target.split(".")
+            m = sys.modules[__name__] if mod == "gen_attn_asm" else importlib.import_module(mod)
+            assert hasattr(m, name), target
+            setattr(m, name, int(val))
     from gen_d128 import gen_dkdv128, gen_dq128
     from gen_fwd128 import gen_fwd128
     from gen_fwd import gen_fwd
