@@ -2034,7 +2034,9 @@ int pw_gemm_launch(const GemmGeom& g, const void* src, const void* wt, void* dst
   const size_t lds = (size_t)NS * row_bytes;
   const int64_t tiles = vd_cdiv(g.M, 16);
   int64_t wgs = vd_cdiv(tiles, 4);
-  const int64_t cap = (int64_t)256 * 8 / slices;  // persistent: <= 8 workgroups per CU in all
+  // persistent: <= 4 workgroups per CU in all (8 measured 4-30 % slower on 6 of the 7 UNet
+  // shapes: fewer waves contend less for the write path; profiles/r05u_prof_conv1x1.md)
+  const int64_t cap = (int64_t)256 * 4 / slices;
   if (wgs > cap) wgs = cap < 256 ? 256 : cap;
   const int64_t ppb = (int64_t)g.dT * g.dH * g.dW;
   dim3 grid((unsigned)wgs, (unsigned)slices);

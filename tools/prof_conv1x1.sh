@@ -1,13 +1,14 @@
 #!/bin/bash
-# Kernel durations of tools/conv1x1_bench.py under rocprofv3, streaming 1x1 kernel off / on.
+# Kernel durations of tools/conv1x1_bench.py under rocprofv3 for each VDIFF_PW_AB value given
+# (default: 0), per (kernel, grid, LDS) shape.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for pw in 0 1; do
-  rm -rf /tmp/prof_pw$pw
-  VDIFF_CONV_PW=$pw timeout -k 10 200 rocprofv3 --kernel-trace -d /tmp/prof_pw$pw -o run -- \
-    python -u tools/conv1x1_bench.py > gpurun_out/pw$pw.log 2>&1 || { tail gpurun_out/pw$pw.log; exit 1; }
-  db=$(find /tmp/prof_pw$pw -name '*.db' | head -n 1)
-  echo "== VDIFF_CONV_PW=$pw"
+for ab in ${@:-0}; do
+  rm -rf /tmp/prof_pw$ab
+  VDIFF_PW_AB=$ab timeout -k 10 200 rocprofv3 --kernel-trace -d /tmp/prof_pw$ab -o run -- \
+    python -u tools/conv1x1_bench.py > gpurun_out/pw$ab.log 2>&1 || { tail gpurun_out/pw$ab.log; exit 1; }
+  db=$(find /tmp/prof_pw$ab -name '*.db' | head -n 1)
+  echo "== VDIFF_PW_AB=$ab"
   python tools/prof_dispatch.py "$db" gemm
 done > gpurun_out/prof_conv1x1.md
 cat gpurun_out/prof_conv1x1.md
