@@ -38,6 +38,9 @@ def test_bench_spawns_two_ranks_train():
     assert ar["steps"] == 2 and ar["standalone_ms_per_step"] > 0
     assert ar["grad_mbytes"] > 500  # UNet3D + wav2vec2-base fp32 gradients (+ flags)
     assert r["value"] > 0
+    st = r["spatial_temporal"]  # the auxiliary leg over both ranks (short temporal kernels)
+    assert st.get("error") is None and st["value"] > 0, st
+    assert st["roofline_temporal"]["achieved"] > 0
 
 
 def test_bench_spawns_two_ranks_vivit_ddp():
