@@ -124,6 +124,7 @@ def train(argv=None):
     loss = torch.zeros(())
     for epoch in range(start_epoch, args.epochs):
         t0 = time.time()
+        loss_sum = torch.zeros((), device=device)  # the epoch's mean loss, summed on the device
         for step in range(args.steps_per_epoch):
             if batcher is not None:
                 clip = batcher.next()
@@ -132,12 +133,14 @@ def train(argv=None):
                                       args.num_timesteps, device,
                                       seed=(epoch * 1000003 + step) * world + rank, dims=args.dims)
             loss = trainer.step(clip)
+            loss_sum += loss
         trainer.check_finite()  # the device-side NaN/Inf record, read once per epoch
         if rank == 0:
             dt = time.time() - t0
             fps = world * args.batch_size * frames * args.steps_per_epoch / dt
-            print(f"Finished epoch {epoch + 1} | Loss: {loss.item()} | {fps:.2f} frames/s",
-                  flush=True)
+            # the reference prints the epoch's last loss (train.py:136); the mean is added
+            print(f"Finished epoch {epoch + 1} | Loss: {loss.item()} | mean "
+                  f"{loss_sum.item() / args.steps_per_epoch:.5f} | {fps:.2f} frames/s", flush=True)
             torch.save(model.state_dict(), args.ckpt)
             torch.save({"model": model.state_dict(), "optimizer": trainer.opt.state_dict(),
                         "epoch": epoch}, args.ckpt + ".resume")
