@@ -878,315 +878,12 @@ __device__ __forceinline__ int wg_off(int r, int c) {  // element offset of chan
   return r * 64 + ((((c >> 3) ^ wg_swz(r)) << 3) | (c & 7));
 }
 
-// The KS form of wgrad_dma_kernel's main loop and epilogue (see there).  Wave w = wk * WCO +
-// wco takes co [64 wco, +64) of the tile and the k-steps kb = wk * (4 / KSN) + kk of every
-// 64-pixel step.  Fragments as in the 16x16x32 form: within each 16-lane group a lane passes
-// (row base + q4, column base + 4 p4) to ds_read_b64_tr_b16 and gets column base + fr of the
-// four rows; 32x32x16 operands: co / ci = 16 (G & 1) + fr, pixels 8 (G >> 1) + 0..7, G = lane / 16.
-template <int RW, int COT, int NST, int PIECES, int STAGE, int Y_BYTES, typename Issue>
-__device__ __forceinline__ void wgrad_ks_body(const WgtGeom& g, int wc, int SW, char* smem,
-                                              const bf16_t* lds, int wave, int lane,
-                                              int nsteps, Issue& issue, float* __restrict__ dw,
-                                              int wsplit, int co0, int ci0, int tab) {
-  constexpr int WCO = COT / 64, KSN = 4 / WCO, KPW = 4 / KSN;
-  const int wco = wave % WCO, wk = wave / WCO;
-  f32x16 acc[3][2][2];
-#pragma unroll
-  for (int tc = 0; tc < 3; ++tc)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[tc][i][j][r] = 0.f;
-  vm_drain();
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s) issue(s);
-  const int G = lane >> 4, fr = lane & 15, q4 = fr >> 2, p4 = fr & 3;
-  for (int s = 0; s < nsteps; ++s) {
-    vm_wait_barrier<(NST - 2) * PIECES>();
-    issue(s + NST - 1);
-    const bf16_t* Ys = lds + (s % NST) * (STAGE / 2);
-    const bf16_t* Xs = Ys + Y_BYTES / 2;
-#pragma unroll
-    for (int kk = 0; kk < KPW; ++kk) {
-      const int kb = wk * KPW + kk;
-      const int p_lo = 16 * kb + 8 * (G >> 1) + q4, p_hi = p_lo + 4;
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int c = wco * 64 + 32 * i + 16 * (G & 1) + 4 * p4;
-        const bf16_t* plane = Ys + (c >> 6) * 4096;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_bf16x4*)(plane + wg_off(p_lo, c & 63)));
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_bf16x4*)(plane + wg_off(p_hi, c & 63)));
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      const int s_lo = (p_lo / wc) * SW + p_lo % wc, s_hi = (p_hi / wc) * SW + p_hi % wc;
-#pragma unroll
-      for (int tc = 0; tc < 3; ++tc) {
-        bf16x8 bfr[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int c = 32 * j + 16 * (G & 1) + 4 * p4;
-          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(Xs + wg_off(s_lo + tc, c)));
-          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(Xs + wg_off(s_hi + tc, c)));
-          bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[tc][i][j] =
-                __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[tc][i][j], 0, 0, 0);
-      }
-    }
-  }
-  vm_drain();
-  __syncthreads();  // every wave is done with the ring: its LDS holds the reduction
-  // per tap: the four waves' 64 x 64 partial tiles [wave][blk = 2 i + j][r][lane] (64 KiB),
-  // then the KSN waves of each co half add theirs in wave order, pair (blk, r) by pair
-  float* red = reinterpret_cast<float*>(smem);
-  const int taps = g.kt * g.kh * g.kw;
-  const int64_t krow = (int64_t)taps * g.Ci;
-#pragma unroll
-  for (int tc = 0; tc < 3; ++tc) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          red[((wave * 4 + 2 * i + j) * 16 + r) * 64 + lane] = acc[tc][i][j][r];
-    __syncthreads();
-    const int tap = tab * g.kw + tc;
-    for (int idx = wk; idx < 64; idx += KSN) {
-      const int blk = idx >> 4, r = idx & 15;
-      float v = red[((wco * 4 + blk) * 16 + r) * 64 + lane];
-#pragma unroll
-      for (int k = 1; k < KSN; ++k) v += red[(((wco + WCO * k) * 4 + blk) * 16 + r) * 64 + lane];
-      const int co = co0 + wco * 64 + 32 * (blk >> 1) + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
-      const int ci = ci0 + 32 * (blk & 1) + (lane & 31);
-      if (co < g.Co && ci < g.Ci)
-        wg_out(g, dw, wsplit, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, v);
-    }
-    __syncthreads();
-  }
-}
-
-// ----------------------------------------------------------- bf16 weight gradient, wide tiles
-// The kw-strip weight gradient with a 128 co x 128 ci x 3-tap workgroup tile (round 4): 8 waves
-// (two per SIMD), wave w = (wco = w & 1, wci = (w >> 1) & 1, wk = w >> 2) owns co [64 wco, +64)
-// x ci [64 wci, +64) x 3 taps (192 fp32 accumulators) over the k-steps 2 wk, 2 wk + 1 (16
-// pixels each, v_mfma_f32_32x32x16_bf16) of every 64-pixel step.  Against the 64 x 64 tile
-// (two 4-wave workgroups per CU) it LDS-DMAs half the bytes per MAC: per step 16 KiB of dY
-// (two 64-channel planes) and 2 x RW x 128 B of X strip for 4x the MACs.  The two k-halves'
-// tiles are added through LDS after the loop, wk = 0 + wk = 1 in that order (fixed).
-// LDS per stage: dY planes [2][64 rows][128 B] | X planes [2][RW rows][128 B].
-template <int RW, int NST>
-__global__ __launch_bounds__(512, 1) void wgrad_wide_kernel(WgtGeom g, int wc,
-                                                            const bf16_t* __restrict__ x,
-                                                            const bf16_t* __restrict__ dy,
-                                                            float* __restrict__ dw) {
-  constexpr int YB = 2 * 64 * 128, XPB = RW * 128, STAGE = YB + 2 * XPB;
-  constexpr int XPP = RW / 8;          // X pieces (1 KiB = 8 rows) per plane
-  constexpr int PY = 2, PX = XPP / 4;  // pieces per wave per step (16 dY, 2 XPP X pieces)
-  static_assert(XPP % 4 == 0, "X pieces split over 8 waves");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const bf16_t* lds = reinterpret_cast<const bf16_t*>(smem);
-
-  const int co_tiles = (g.Co + 127) / 128, ci_tiles = (g.Ci + 127) / 128;
-  int bid, wsplit;
-  if (!wg_tile(g, &bid, &wsplit)) return;
-  const int cot = bid % co_tiles; bid /= co_tiles;
-  const int cit = bid % ci_tiles; bid /= ci_tiles;
-  const int tab = bid, ta = tab / g.kh, tb = tab % g.kh;
-  const int co0 = cot * 128, ci0 = cit * 128;
-  const int64_t mbeg = (int64_t)wsplit * g.m_per_split;
-  int64_t mend = mbeg + g.m_per_split;
-  if (mend > g.M) mend = g.M;
-  if (mbeg >= mend) return;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane >> 3, pc = lane & 7;
-  const int SW = wc + 2;
-  // the pieces' lane constants are recomputed at every issue (registers: 192 accumulators
-  // at two waves per SIMD leave ~64): dY piece pi = 2 wave + i: plane pi >> 3, pixel row
-  // (pi & 7) * 8 + lr; X piece pi = PX wave + i: plane pi / XPP, strip row (pi % XPP) * 8 + lr
-  const rsrc_t rs_y = make_rsrc(dy, (uint32_t)(g.M * g.yCs * 2));
-  const rsrc_t rs_x = make_rsrc(x, (uint32_t)((int64_t)g.B * g.Ti * g.Hi * g.Wi * g.xCs * 2));
-  int cb, ct, chh, cw;
-  {
-    int64_t m = mbeg;
-    cw = (int)(m % g.Wo); m /= g.Wo;
-    chh = (int)(m % g.Ho); m /= g.Ho;
-    ct = (int)(m % g.To);
-    cb = (int)(m / g.To);
-  }
-  const int nsteps = (int)((mend - mbeg + 63) / 64);
-  auto issue = [&](int s) {
-    char* st = smem + (s % NST) * STAGE;
-    const bool live = s < nsteps;
-    const int ms = (int)mbeg + s * 64, me = (int)mend;
-#pragma unroll
-    for (int i = 0; i < PY; ++i) {
-      const int pi = wave * PY + i;
-      const int yp = (pi & 7) * 8 + lr;
-      const int ycol = co0 + (pi >> 3) * 64 + (pc ^ wg_swz(yp)) * 8;
-      const bool ok = live & (ms + yp < me) & (ycol < g.Co);
-      dma_lds<16>(rs_y, lds_addr(st + pi * 1024),
-                  ok ? (uint32_t)(((ms + yp) * g.yCs + ycol) * 2) : 0x80000000u);
-    }
-#pragma unroll
-    for (int i = 0; i < PX; ++i) {
-      const int pi = wave * PX + i;
-      const int plane = pi / XPP, q = pi % XPP;
-      const int sr = q * 8 + lr;
-      int xrr = sr / SW;
-      const int xj = sr - xrr * SW;
-      if (xrr >= 64 / wc) xrr = -1;
-      const int xcol = ci0 + plane * 64 + (pc ^ wg_swz(sr)) * 8;
-      uint32_t off = 0x80000000u;
-      if (live & (xrr >= 0) & (xcol < g.Ci)) {
-        int b = cb, t = ct, h = chh + xrr;
-        while (h >= g.Ho) {
-          h -= g.Ho;
-          if (++t == g.To) {
-            t = 0;
-            ++b;
-          }
-        }
-        const int ti = t - g.pt + ta, hi = h - g.ph + tb, wi = cw + xj - g.pw;
-        if (b < g.B && (unsigned)ti < (unsigned)g.Ti && (unsigned)hi < (unsigned)g.Hi &&
-            (unsigned)wi < (unsigned)g.Wi) {
-          const int pix = ((b * g.Ti + ti) * g.Hi + hi) * g.Wi + wi;
-          off = (uint32_t)((pix * g.xCs + xcol) * 2);
-        }
-      }
-      dma_lds<16>(rs_x, lds_addr(st + YB + plane * XPB + q * 1024), off);
-    }
-    if (live) {
-      cw += 64;
-      while (cw >= g.Wo) {
-        cw -= g.Wo;
-        if (++chh == g.Ho) {
-          chh = 0;
-          if (++ct == g.To) {
-            ct = 0;
-            ++cb;
-          }
-        }
-      }
-    }
-  };
-
-  const int wco = wave & 1, wci = (wave >> 1) & 1, wk = wave >> 2;
-  f32x16 acc[3][2][2];
-#pragma unroll
-  for (int tc = 0; tc < 3; ++tc)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[tc][i][j][r] = 0.f;
-  vm_drain();
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s) issue(s);
-  const int G = lane >> 4, fr = lane & 15, q4 = fr >> 2, p4 = fr & 3;
-  for (int s = 0; s < nsteps; ++s) {
-    vm_wait_barrier<(NST - 2) * (PY + PX)>();
-    issue(s + NST - 1);
-    const bf16_t* Ys = lds + (s % NST) * (STAGE / 2) + wco * 4096;
-    const bf16_t* Xs = lds + (s % NST) * (STAGE / 2) + YB / 2 + wci * (XPB / 2);
-#pragma unroll 1
-    for (int kk = 0; kk < 2; ++kk) {
-      const int p_lo = 16 * (2 * wk + kk) + 8 * (G >> 1) + q4, p_hi = p_lo + 4;
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int c = 32 * i + 16 * (G & 1) + 4 * p4;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Ys + wg_off(p_lo, c)));
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Ys + wg_off(p_hi, c)));
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      const int s_lo = (p_lo / wc) * SW + p_lo % wc, s_hi = (p_hi / wc) * SW + p_hi % wc;
-#pragma unroll
-      for (int tc = 0; tc < 3; ++tc) {
-        bf16x8 bfr[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int c = 32 * j + 16 * (G & 1) + 4 * p4;
-          const bf16x4 lo =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Xs + wg_off(s_lo + tc, c)));
-          const bf16x4 hi =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Xs + wg_off(s_hi + tc, c)));
-          bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[tc][i][j] =
-                __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[tc][i][j], 0, 0, 0);
-      }
-    }
-  }
-  vm_drain();
-  __syncthreads();  // the ring is free: its LDS holds the k-half reduction
-  float* red = reinterpret_cast<float*>(smem);  // [4 (wco, wci)][4 blk][16 r][64 lanes]
-  const int taps = g.kt * g.kh * g.kw;
-  const int64_t krow = (int64_t)taps * g.Ci;
-  const int pair = wave & 3;
-#pragma unroll
-  for (int tc = 0; tc < 3; ++tc) {
-    if (wk == 1) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            red[((pair * 4 + 2 * i + j) * 16 + r) * 64 + lane] = acc[tc][i][j][r];
-    }
-    __syncthreads();
-    if (wk == 0) {
-      const int tap = tab * g.kw + tc;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int ci = ci0 + wci * 64 + 32 * j + (lane & 31);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float v = acc[tc][i][j][r] + red[((pair * 4 + 2 * i + j) * 16 + r) * 64 + lane];
-            const int co = co0 + wco * 64 + 32 * i + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
-            if (co < g.Co && ci < g.Ci)
-              wg_out(g, dw, wsplit, (int64_t)co * krow + (int64_t)tap * g.Ci + ci, v);
-          }
-        }
-    }
-    __syncthreads();
-  }
-}
-
 // PLANE (round 2): all nine (kh, kw) taps of one kt per workgroup -- the X strip holds the
 // three input rows above / at / below the step's 64-pixel output row (W % 64 == 0, so a step
 // is one row segment), and one dY tile feeds nine taps instead of three.
 //
-// KS (round 4): the four waves split each 64-pixel step's reduction (16 pixels = one k-step
-// of v_mfma_f32_32x32x16_bf16 each, COT = 64; COT = 128: two co halves x two k-halves)
-// instead of the output tile, so every wave owns a 64 co x 64 ci x 3-tap tile (192 fp32
-// accumulators, one wave per SIMD).  Per 384 MFMA cycles a wave then reads 8 KiB of
-// transposed fragments instead of 16 KiB: the COT = 64 form needs 128 B/clk of LDS per CU at
-// the MFMA rate (two workgroups per CU), the LDS peak, and is LDS-bound; this one needs 64.
-// The waves' partial tiles are added through LDS after the loop, in wave order (fixed).
-template <int RW, int COT, int NST, bool ONE, bool PLANE = false, bool KS = false>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
-__global__ __launch_bounds__(kThreads, (PLANE || KS) ? 1 : 2) void wgrad_dma_kernel(
+template <int RW, int COT, int NST, bool ONE, bool PLANE = false>  // ONE: 1x1 stride-1 unpadded conv, X rows = dY rows
+__global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
     WgtGeom g, int wc, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
     float* __restrict__ dw) {
   constexpr int PY = COT / 32, PX = RW / 32;  // pieces per wave per step
@@ -1312,12 +1009,6 @@ __global__ __launch_bounds__(kThreads, (PLANE || KS) ? 1 : 2) void wgrad_dma_ker
     }
   };
 
-  if constexpr (KS) {
-    static_assert(!ONE && !PLANE && (COT == 64 || COT == 128), "KS: kw-strip tiles");
-    wgrad_ks_body<RW, COT, NST, PIECES, STAGE, Y_BYTES>(g, wc, SW, smem, lds, wave, lane, nsteps,
-                                                        issue, dw, wsplit, co0, ci0, tab);
-    return;
-  }
   // wave tile: co [WTM wm, +WTM) x ci [32 wn, +32) x 3 taps
   const int wm = wave & 1, wn = wave >> 1;
   f32x4 acc[NT][NI][2];
@@ -1626,7 +1317,7 @@ constexpr int kHaT = kHoT + 2, kHaH = kHoH + 2, kHaW = kHoW + 2;  // input halo
 constexpr int kHaP = kHaT * kHaH * kHaW;                         // 432 pixels = 54 pieces
 // KS channels per step: 64 (128-B LDS rows, 80 KiB per workgroup, two per CU) or 32 (64-B
 // rows, 40 KiB, four per CU); weight ring stages NSTB (prefetch distance NSTB - 1):
-// VDIFF_CONV_HALO_KS / VDIFF_CONV_HALO_ST select them (A/B).
+// VDIFF_CONV_HALO_KS forces the channel step (A/B).
 template <int NSTB, int KS>
 constexpr size_t halo_lds() { return (size_t)(kHaP + NSTB * 64) * 2 * KS + 1024; }  // + junk
 static_assert(kHaP % 16 == 0, "whole halo pieces");
@@ -1825,7 +1516,7 @@ bool halo_ok(const GemmGeom& g) {
 // 0.84x) and at the 32x32 level up to N = 256 (0.68-0.83x); with N >= 128 at 64x64 and
 // 128x128 the gathered 128 x 128 tiles keep the edge (1.0-1.1x): the halo kernel's N tile is
 // 64, so every 64 output channels re-load the halo.  Deeper weight rings (one workgroup per
-// CU) and 8 waves per workgroup measured slower (VDIFF_CONV_HALO_ST / _NW).
+// CU) and 8 waves per workgroup measured slower (removed in round 5).
 std::atomic<int> g_halo_mode{[] {
   const char* e = getenv("VDIFF_CONV_HALO");
   return e ? atoi(e) : 2;
@@ -1863,35 +1554,13 @@ void launch_halo_st(const GemmGeom& g, const void* src, const void* wt, void* ds
   kern<<<grid, 64 * NW, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias,
                                    ca, (const bf16_t*)res);
 }
-int conv_halo_waves() {
-  static const int v = [] {
-    const char* e = getenv("VDIFF_CONV_HALO_NW");
-    return e ? atoi(e) : 4;
-  }();
-  return v;
-}
-int conv_halo_stages() {
-  static const int v = [] {
-    const char* e = getenv("VDIFF_CONV_HALO_ST");
-    return e ? atoi(e) : 3;
-  }();
-  return v;
-}
+// (8 waves per workgroup, a 5-stage weight ring and a 4-frame tile measured slower: DESIGN
+// section 4; removed)
 template <bool TR>
 void launch_halo(const GemmGeom& g, int ks, const void* src, const void* wt, void* dst,
                  const float* bias, const float* ca, const void* res, hipStream_t st) {
-  const int ns = conv_halo_stages();
-  if (ks == 32) {
-    launch_halo_st<TR, 3, 4, 32>(g, src, wt, dst, bias, ca, res, st);
-    return;
-  }
-  if (conv_halo_waves() == 8) {
-    if (ns == 5) launch_halo_st<TR, 5, 8>(g, src, wt, dst, bias, ca, res, st);
-    else launch_halo_st<TR, 3, 8>(g, src, wt, dst, bias, ca, res, st);
-  } else {
-    if (ns == 5) launch_halo_st<TR, 5, 4>(g, src, wt, dst, bias, ca, res, st);
-    else launch_halo_st<TR, 3, 4>(g, src, wt, dst, bias, ca, res, st);
-  }
+  if (ks == 32) launch_halo_st<TR, 3, 4, 32>(g, src, wt, dst, bias, ca, res, st);
+  else launch_halo_st<TR, 3, 4>(g, src, wt, dst, bias, ca, res, st);
 }
 
 // ----------------------------------------------------------------- 1x1 convs: streaming GEMM
@@ -2319,28 +1988,16 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
       return e ? atoi(e) : 0;
     }();
     const bool plane = !one && wplane && d->Wo % 64 == 0;
-    // K-split waves for the kw-strip tiles (wgrad_ks_body; A/B knob VDIFF_WGRAD_KS)
-    static const int wks = [] {
-      const char* e = getenv("VDIFF_WGRAD_KS");
-      return e ? atoi(e) : 0;
-    }();
-    // 128 x 128 workgroup tiles of 8 waves (wgrad_wide_kernel; A/B knob VDIFF_WGRAD_WIDE=1:
-    // about two workgroups per CU, =2: one)
-    static const int wwide = [] {
-      const char* e = getenv("VDIFF_WGRAD_WIDE");
-      return e ? atoi(e) : 0;
-    }();
-    const bool wide = wwide && !one && !plane && !wks && d->Co >= 128 && d->Ci >= 128;
-    const int64_t tiles = wide ? (int64_t)vd_cdiv(d->Co, 128) * vd_cdiv(d->Ci, 128) * d->kt * d->kh
-                               : (int64_t)vd_cdiv(d->Co, cot) * vd_cdiv(d->Ci, 64) *
-                                     (one ? 1 : (plane ? d->kt : d->kt * d->kh));
+    // (the K-split-wave and 128 x 128-tile forms of round 4 measured slower on every shape:
+    // DESIGN section 4, removed in round 5)
+    const int64_t tiles = (int64_t)vd_cdiv(d->Co, cot) * vd_cdiv(d->Ci, 64) *
+                          (one ? 1 : (plane ? d->kt : d->kt * d->kh));
     // ~2048 workgroups, but at least 32 K steps each for the strip kernel (shorter pixel
     // ranges lose more to the ring's fill and the atomic epilogue than they gain in
     // occupancy: 64->64 at 128x128 0.13 -> 0.116 ms, tools/conv_ab.sh); planes do three
-    // times the MFMA work per step: at least 16 steps; wide tiles (one workgroup per CU):
-    // about two workgroups per CU, at least 16 steps each
-    int64_t splits = vd_cdiv(wide ? (wwide == 2 ? 256 : 512) : 2048, tiles);
-    int64_t maxs = vd_cdiv(g.M, (one || plane || wide) ? 1024 : 64 * w3_msteps);
+    // times the MFMA work per step: at least 16 steps
+    int64_t splits = vd_cdiv(2048, tiles);
+    int64_t maxs = vd_cdiv(g.M, (one || plane) ? 1024 : 64 * w3_msteps);
     if (splits > maxs) splits = maxs;
     // occupancy rounds (default since round 4; VDIFF_WGRAD_QRULE=0 turns it off, =c applies
     // it only where the rule above gives at most c splits): the grid of equal-length
@@ -2353,7 +2010,7 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
       const char* e = getenv("VDIFF_WGRAD_QRULE");
       return e ? atoi(e) : (1 << 30);
     }();
-    if (wq > 0 && splits <= wq && !wide && !plane && !wks) {
+    if (wq > 0 && splits <= wq && !plane) {
       // resident workgroups per CU: LDS ring (160 KiB per CU) and registers (3 per CU for
       // the kw strip's 134-136 VGPRs)
       const int nst = one ? (cot >= 128 ? (w1_nst >= 4 ? 4 : 2)
@@ -2399,34 +2056,14 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
 #define VD_WGD(RW, COT, NST, ONE, ...)                                                     \
   do {                                                                                     \
     auto kern = wgrad_dma_kernel<RW, COT, NST, ONE, ##__VA_ARGS__>;                        \
-    const int lds = std::max(NST * (COT + RW) * 128, wks ? 65536 : 0);                     \
+    const int lds = NST * (COT + RW) * 128;                                                \
     (void)hipFuncSetAttribute((const void*)kern,                                           \
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
     kern<<<grid, kThreads, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);     \
   } while (0)
     // 64 x 64 tiles, double-buffered (40 KiB at RW = 96: three workgroups per CU).
     // Measured against COT = 128 and a three-stage ring: both slower (tools/conv_ab.sh).
-    if (wide) {
-      const int rows_w = (64 / wc) * (wc + 2);
-      auto launch_wide = [&](auto kern, int lds) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds);
-        kern<<<grid, 512, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);
-      };
-      if (rows_w <= 96) launch_wide(wgrad_wide_kernel<96, 2>, 2 * (16384 + 2 * 96 * 128));
-      else if (rows_w <= 128) launch_wide(wgrad_wide_kernel<128, 2>, 2 * (16384 + 2 * 128 * 128));
-      else launch_wide(wgrad_wide_kernel<192, 2>, std::max(2 * (16384 + 2 * 192 * 128), 65536));
-      return vd::check_launch("conv_wgrad_wide");
-    }
-    if (wks && !one && !plane) {  // K-split waves (A/B: VDIFF_WGRAD_KS=1)
-      if (cot == 128 && rows <= 96) VD_WGD(96, 128, 3, false, false, true);
-      else if (cot == 128 && rows <= 128) VD_WGD(128, 128, 3, false, false, true);
-      else if (cot == 128) VD_WGD(192, 128, 3, false, false, true);
-      else if (rows <= 96) VD_WGD(96, 64, 4, false, false, true);
-      else if (rows <= 128) VD_WGD(128, 64, 4, false, false, true);
-      else VD_WGD(192, 64, 3, false, false, true);
-    }
-    else if (one && cot == 192 && w1_nst >= 4) VD_WGD(64, 192, 4, true);
+    if (one && cot == 192 && w1_nst >= 4) VD_WGD(64, 192, 4, true);
     else if (one && cot == 192) VD_WGD(64, 192, 2, true);
     else if (one && cot == 128 && w1_nst >= 4) VD_WGD(64, 128, 4, true);
     else if (one && cot == 128) VD_WGD(64, 128, 2, true);

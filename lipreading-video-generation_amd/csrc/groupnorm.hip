@@ -27,9 +27,8 @@ static int env_int(const char* name, int dflt) {
 }
 const int kTargetChunks = env_int("VDIFF_GN_CHUNKS", 1024);
 const int kSumPer = env_int("VDIFF_GN_SUMPER", 64);
-// pixel rows whose loads each thread keeps in flight before using them (VDIFF_GN_UNROLL 1, 2, 4;
-// the per-row arithmetic and the accumulation order are unchanged)
-const int kUnroll = env_int("VDIFF_GN_UNROLL", 1) >= 4 ? 4 : (env_int("VDIFF_GN_UNROLL", 1) >= 2 ? 2 : 1);
+// The kernels take U, the pixel rows whose loads each thread keeps in flight; U = 2 / 4 measured
+// equal or slower (round 4) and only U = 1 is launched since round 5.
 
 struct GNPlan {
   int rows_per_iter;  // pixel rows a WG covers per iteration
@@ -535,13 +534,7 @@ int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, 
                                                             rstd, (T*)y, S, C, G, p.chunk_px,   \
                                                             p.rows_per_iter, drop)
   return VD_DISPATCH_DTYPE(dtype, T, {
-    if (kUnroll == 4) {
-      VD_GN_FWD(4);
-    } else if (kUnroll == 2) {
-      VD_GN_FWD(2);
-    } else {
-      VD_GN_FWD(1);
-    }
+    VD_GN_FWD(1);
   });
 #undef VD_GN_FWD
 }
@@ -586,13 +579,7 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
         (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,   \
         p.rows_per_iter, drop)
   return VD_DISPATCH_DTYPE(dtype, T, {
-    if (kUnroll == 4) {
-      VD_GN_BWD(4);
-    } else if (kUnroll == 2) {
-      VD_GN_BWD(2);
-    } else {
-      VD_GN_BWD(1);
-    }
+    VD_GN_BWD(1);
   });
 #undef VD_GN_BWD
 }

@@ -16,7 +16,7 @@ from vdiff import _lib, ops
 import torch
 
 ENV = ("VDIFF_WGRAD1", "VDIFF_WGRAD3", "VDIFF_WGRAD_QRULE", "VDIFF_WGRAD_SPLITS",
-       "VDIFF_WGRAD_WIDE", "VDIFF_WGRAD_KS", "VDIFF_CONV_WPLANE", "VDIFF_ASM256_FWD",
+       "VDIFF_CONV_WPLANE", "VDIFF_ASM256_FWD",
        "VDIFF_ATTN_CFG", "VDIFF_CONV_DMA", "VDIFF_CONV_LEGACY")
 pytestmark = pytest.mark.skipif(any(os.environ.get(e) for e in ENV),
                                 reason="non-default kernel-selection environment")

@@ -3,8 +3,8 @@
 vd_conv3d_bwd_weight_det (fixed-order split-K, the default) or vd_conv3d_bwd_weight (atomics,
 VDIFF_WGRAD_ATOMIC=1), timed with HIP events; the grid layout follows VDIFF_WGRAD_XCD (read
 once per process).  Checked against the fp32 parity-mode weight gradient of the same values on
-the device (whole tensors).  Prints per-shape microseconds / TFLOP/s and the per-step totals.  VDIFF_WGRAD_KS=1 selects the K-split-wave kw-strip kernel (wgrad_ks_body).
-    VDIFF_WGRAD_XCD=0|1 [VDIFF_WGRAD_ATOMIC=1] [VDIFF_WGRAD_KS=1] python tools/wgrad_ab.py"""
+the device (whole tensors).  Prints per-shape microseconds / TFLOP/s and the per-step totals.
+    VDIFF_WGRAD_XCD=0|1 [VDIFF_WGRAD_ATOMIC=1] python tools/wgrad_ab.py"""
 import os
 import sys
 
@@ -28,9 +28,7 @@ SHAPES = ((256, 256, 3, 32, 16, 10), (64, 64, 3, 128, 16, 7), (128, 128, 3, 64, 
 
 def main():
     atomic = os.environ.get("VDIFF_WGRAD_ATOMIC", "0") == "1"
-    tag = (f"xcd={os.environ.get('VDIFF_WGRAD_XCD', '1')} {'atomic' if atomic else 'det'}"
-           f"{' ks' if os.environ.get('VDIFF_WGRAD_KS', '0') == '1' else ''}"
-           f"{' wide' if os.environ.get('VDIFF_WGRAD_WIDE', '0') == '1' else ''}")
+    tag = f"xcd={os.environ.get('VDIFF_WGRAD_XCD', '1')} {'atomic' if atomic else 'det'}"
     tot3 = tot1 = 0.0
     worst = 0.0
     for Ci, Co, k, H, T, per in SHAPES:
