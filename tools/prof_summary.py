@@ -42,13 +42,14 @@ def from_db(path, by_grid=False):
 
 def unit_line(path):
     """The bench's roofline unit (the head_dim-64 backward pair at N = 262144, one sequence per
-    launch: 8 N^2 D algorithmic FLOP) from the launches of ONE grid shape per kernel -- the
-    grid with the largest total time (the headline's N = 262144 launches; the auxiliary
-    spatial_temporal leg runs the same kernels per frame at N = 16384 on other grids)."""
+    launch: 8 N^2 D algorithmic FLOP) from the launches of that grid only, (262144, 1, 1) in
+    threads (the auxiliary spatial_temporal leg runs the same kernels per frame at N = 16384
+    on other grids); None when the process ran no such launch."""
     rows = from_db(path, by_grid=True)
     best = {}
     for (name, grid), r in rows.items():
-        if name in ("vd_attn_bwd_dq_d64", "vd_attn_bwd_dkdv_d64"):
+        # one N = 262144 sequence per launch: 1024 workgroups of 256 threads, z = 1
+        if name in ("vd_attn_bwd_dq_d64", "vd_attn_bwd_dkdv_d64") and tuple(grid[:3]) == (262144, 1, 1):
             if name not in best or r[1] > best[name][1][1]:
                 best[name] = (grid, r)
     if len(best) < 2:
