@@ -18,7 +18,7 @@ from dataclasses import dataclass
 
 import torch
 
-from . import ops
+from . import hipgraph, ops
 from .ddp import GradBucketer
 
 
@@ -278,7 +278,7 @@ class TrainStepGraph:
         lib = _lib.lib()
         lib.vd_set_dropout_counter(self.ctr.data_ptr())
         try:
-            with torch.cuda.graph(self.g, capture_error_mode="thread_local"):
+            with hipgraph.capture(self.g, capture_error_mode="thread_local"):
                 self.ctr.add_(1)
                 self._body()
         finally:
@@ -341,7 +341,7 @@ class DDIMGraph:
             self.xt.copy_(keep)
         cur.wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with hipgraph.capture(self.graph):
             self.x0 = self._body()
 
     def step(self, i):

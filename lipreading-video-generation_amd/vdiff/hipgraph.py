@@ -3,7 +3,11 @@ libamdhip64.so): node types, and for memset nodes the destination, size and valu
 diagnostic: TrainStepGraph.node_types(), the graph-replay tests (no memset node may sit in a
 captured train step) and tools/graph_reduce_repro.py.  torch: capture with torch.cuda.CUDAGraph(keep_graph=True)
 and pass graph.raw_cuda_graph()."""
+import contextlib
 import ctypes
+import gc
+
+import torch
 
 NODE_TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "graph", 5: "empty",
               6: "wait_event", 7: "event_record", 8: "ext_semas_signal", 9: "ext_semas_wait",
@@ -59,3 +63,21 @@ def read_i32(dev_ptr, count=1):
     _check(hip().hipMemcpy(buf, ctypes.c_void_p(dev_ptr), ctypes.c_size_t(4 * count), 2),
            "hipMemcpy")
     return list(buf)
+
+
+@contextlib.contextmanager
+def capture(graph, **kw):
+    """torch.cuda.graph(graph, **kw) with Python's garbage collector off for the capture.
+    torch collects once before capturing, but a collection triggered by allocations DURING
+    the capture runs finalizers on the capturing thread, and a finalizer that calls a HIP API
+    a capture forbids aborts the process (seen once in the -m gpu suite, round 5: 'Fatal
+    Python error: Aborted' under 'Garbage-collecting' inside TrainStepGraph._capture)."""
+    enabled = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph, **kw):
+            yield
+    finally:
+        if enabled:
+            gc.enable()

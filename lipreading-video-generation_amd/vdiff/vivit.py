@@ -28,7 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import hipgraph, ops
 
 
 @dataclass
@@ -318,7 +318,7 @@ class VivitTrainer:
         self.opt.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph(keep_graph=True)  # node list kept (node_types)
         if not self.distributed:
-            with torch.cuda.graph(self.graph):
+            with hipgraph.capture(self.graph):
                 self.static_loss = self._step(self.static_x, self.static_y, zero=False)
             self.graph.instantiate()
             self._restore(snapshot)
@@ -327,12 +327,12 @@ class VivitTrainer:
         # thread_local: the process group's watchdog thread may query events meanwhile.
         torch.cuda.synchronize(dev)
         torch.distributed.barrier()
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+        with hipgraph.capture(self.graph, capture_error_mode="thread_local"):
             self.static_loss = self._fwd_bwd(self.static_x, self.static_y)
             grads = [p.grad for p in self.params if p.grad is not None]
             self.flat = torch.cat([g.reshape(-1).float() for g in grads])
         self.graph_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_opt, capture_error_mode="thread_local"):
+        with hipgraph.capture(self.graph_opt, capture_error_mode="thread_local"):
             views = self.flat.split([g.numel() for g in grads])
             torch._foreach_mul_(list(views), 1.0 / self.world)
             torch._foreach_copy_(grads, [v.view_as(g) for v, g in zip(views, grads)])
