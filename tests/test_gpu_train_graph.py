@@ -336,3 +336,22 @@ def test_graph_config2_dropout_replays():
         assert v == v and v >= 0.0, (i, v)
         assert 0.5 * lo <= v <= 2.0 * hi, (i, v, eager)
     assert len(set(graph[2:])) == 3, graph
+
+
+def test_capture_runs_without_garbage_collection():
+    """vdiff.hipgraph.capture keeps Python's collector off while the capture runs (a
+    collection inside a capture runs finalizers on the capturing thread) and restores it."""
+    import gc
+    from vdiff import hipgraph
+    x = torch.zeros(1024, device="cuda")
+    seen = []
+    g = torch.cuda.CUDAGraph()
+    assert gc.isenabled()
+    with hipgraph.capture(g):
+        seen.append(gc.isenabled())
+        x.add_(1.0)
+    assert seen == [False] and gc.isenabled()
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x[0]) == 2.0
