@@ -464,7 +464,7 @@ def short_attention_roofline(summary):
         avg_s = tot_ms / cnt / 1e3
         nb = short_attention_bytes(kind, n, hd, nseq)
         lp = 16 if n <= 16 else 32
-        ex = attention_kernel_flops(kind, lp, hd, nseq) * (5.0 / 7.0 if kind == "attn_bwd" else 1)
+        ex = attention_kernel_flops(kind, lp, hd, nseq)
         alg = (2 if kind == "attn_fwd" else 4) * 2.0 * nseq * n * n * hd
         rows.append({"kernel": "short " + kind.replace("attn_", ""), "head_dim": hd, "seq_len": n,
                      "nseq": nseq, "launches": cnt, "total_ms": round(tot_ms, 3),

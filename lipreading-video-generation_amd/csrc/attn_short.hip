@@ -12,11 +12,13 @@
 //     accumulator rows x 4 lane groups), O^T = V^T P^T (v_mfma_f32_16x16x16_bf16) with V^T
 //     read from the wave's own LDS copy of the V rows by ds_read_b64_tr_b16;
 //   * backward, fused (dQ, dK, dV of the sequence in one wave, no atomics, no partials):
-//     S^T and dP^T once (query on the lane column), delta = rowsum(dO * O) in the kernel,
+//     S^T and dP^T once (query on the lane column), delta = rowsum(P * dP) from them (no O
+//     read),
 //     dQ^T = K^T dS^T from registers, dK^T = Q^T dS and dV^T = dO^T P with P and dS turned
 //     key-on-lane through LDS; Q / K / dO rows in LDS for the transposed operands: 5
 //     products for the 4 algorithmic ones.
-// The bytes are the sequence's q | k | v rows in and o (+ lse) out -- 8 FLOP per byte at
+// The bytes are the sequence's q | k | v rows in and o (+ lse) out (backward: q, k, v, dO,
+// lse in, dq, dk, dv out) -- 8 FLOP per byte at
 // T = 16, D = 64: HBM-bound.  The waves of a workgroup take consecutive
 // sequences, i.e. neighbouring pixels, whose token rows are adjacent in the channels-last
 // qkv buffer.  No barrier: each wave has its own LDS region.
@@ -34,7 +36,7 @@ struct ShortArgs {
   const bf16_t* q;
   const bf16_t* k;
   const bf16_t* v;
-  const bf16_t* o;      // backward: the forward output (delta)
+  const bf16_t* o;      // backward: the forward output (unused: delta from P and dP)
   const bf16_t* dout;   // backward
   bf16_t* out;          // forward: o; backward: dq
   bf16_t* dk;
@@ -257,16 +259,13 @@ __global__ void __launch_bounds__(64 * WPB) short_attn_bwd_kernel(ShortArgs a) {
   const int64_t base = seq_off(s, a.groups, a.bs, a.gs);
   const int64_t obase = seq_off(s, a.groups, a.obs, a.ogs);
   const bf16_t *qp = a.q + base, *kp = a.k + base, *vp = a.v + base;
-  const bf16_t *opp = a.o + obase, *dop = a.dout + obase;
+  const bf16_t* dop = a.dout + obase;
 
   f32x4 sx[NB][NB], px[NB][NB];  // [kb][qb]: column = query, rows = keys
 #pragma unroll
   for (int i = 0; i < NB; ++i)
 #pragma unroll
     for (int j = 0; j < NB; ++j) sx[i][j] = px[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dl[NB];  // partial rowsum(dO * O) of query 16 qb + col over this lane group's columns
-#pragma unroll
-  for (int b = 0; b < NB; ++b) dl[b] = 0.f;
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int c = ks * 32 + 8 * grp;
@@ -279,13 +278,9 @@ __global__ void __launch_bounds__(64 * WPB) short_attn_bwd_kernel(ShortArgs a) {
       kf[b] = ld16(kp + (int64_t)r * a.ts + c, ok);
       vf[b] = ld16(vp + (int64_t)r * a.ts + c, ok);
       df[b] = ld16(dop + (int64_t)r * a.ots + c, ok);
-      const bf16x8 of = ld16(opp + (int64_t)r * a.ots + c, ok);
       st_frag<D>(qt, r, c, qf[b]);
       st_frag<D>(kt, r, c, kf[b]);
       st_frag<D>(dt, r, c, df[b]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        dl[b] = fmaf(bf2f((bf16_t)df[b][j]), bf2f((bf16_t)of[j]), dl[b]);
     }
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb)
@@ -300,17 +295,27 @@ __global__ void __launch_bounds__(64 * WPB) short_attn_bwd_kernel(ShortArgs a) {
 #pragma unroll
   for (int qb = 0; qb < NB; ++qb) {
     const int qr = 16 * qb + col;
-    const float del = bsum4(dl[qb]);
     const float lse2 = qr < L ? a.lse[(int64_t)s * L + qr] * kLog2eS : 0.f;
+    // P of the query's whole row (all its keys are in this wave), then the softmax backward
+    // dS = P (dP - rowsum(P dP)) -- the reference's autograd of softmax -- so the backward
+    // never reads O (FA's rowsum(dO O) is the same sum when O = P V)
+    f32x4 pr[NB];
+    float del = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < NB; ++kb) {
-      f32x4 p, d;
+    for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int key = 16 * kb + 4 * grp + i;
-        p[i] = (key < L && qr < L) ? exp2f(sx[kb][qb][i] * c2 - lse2) : 0.f;
-        d[i] = p[i] * (px[kb][qb][i] - del);
+        pr[kb][i] = (key < L && qr < L) ? exp2f(sx[kb][qb][i] * c2 - lse2) : 0.f;
+        del = fmaf(pr[kb][i], px[kb][qb][i], del);
       }
+    del = bsum4(del);
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      const f32x4 p = pr[kb];
+      f32x4 d;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = p[i] * (px[kb][qb][i] - del);
       const bf16x4 pb = pack4(p);
       dsx[kb][qb] = pack4(d);
       // [query][key] images: this lane's 4 keys are 4 consecutive elements of row qr

@@ -103,10 +103,10 @@ def attention_kernel_flops(kind: str, n: int, ch: int, nseq: int) -> float:
     fwd = 2 products (QK^T, PV); bwd dQ = 3 (QK^T and dO V^T recomputed, dS K);
     bwd dK/dV = 4 (QK^T, dO V^T, dO^T P, dS^T Q).  Each product = 2*n*n*ch per sequence.
     The backward pair therefore executes 7 products against 4 algorithmic ones.  "bwd" is the
-    fused short-sequence backward (attn_short.hip): S and dP in both orientations, dQ, dK,
-    dV = 7 products over the sequence padded to 16 / 32 tokens."""
+    fused short-sequence backward (attn_short.hip): S and dP once, dQ, dK, dV = 5 products
+    over the sequence padded to 16 / 32 tokens."""
     kind = kind.replace("attn_", "")
-    products = {"fwd": 2, "bwd_dq": 3, "bwd_dkdv": 4, "bwd": 7}[kind]
+    products = {"fwd": 2, "bwd_dq": 3, "bwd_dkdv": 4, "bwd": 5}[kind]
     return products * 2.0 * nseq * n * n * ch
 
 
@@ -114,8 +114,9 @@ def short_attention_bytes(kind: str, n: int, ch: int, nseq: int, elem: int = 2) 
     """ALGORITHMIC HBM bytes of one short-sequence attention launch (attn_short.hip; the bound
     of the temporal attention, 16 tokens per sequence): forward reads q, k, v and writes o
     (4 rows of ch elements per token) plus the fp32 log-sum-exp; the fused backward reads q,
-    k, v, o, dO and lse and writes dq, dk, dv (8 rows per token)."""
-    rows = {"fwd": 4, "bwd": 8}[kind.replace("attn_", "")]
+    k, v, dO and lse and writes dq, dk, dv (7 rows per token: since round 5 it takes
+    delta = rowsum(P dP) from the scores it holds instead of reading o)."""
+    rows = {"fwd": 4, "bwd": 7}[kind.replace("attn_", "")]
     return float(nseq) * n * (rows * ch * elem + 4)
 
 
