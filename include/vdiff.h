@@ -310,7 +310,8 @@ int vd_attention_set_config(int cfg);
  * temporal attention of the spatial_temporal mode, T = 16 / 25 frames per pixel, and the
  * ViViT encoder's 9 tokens) run on dedicated kernels, one wave per sequence with 16x16 MFMA
  * tiles: vd_attention_fwd / _fwd_ws, and vd_attention_bwd as ONE fused dQ / dK / dV kernel
- * (no workspace used).  vd_attention_short_path(d) says whether d takes that path;
+ * (no workspace used; it takes delta = rowsum(P dP) from the scores it holds, so its `o`
+ * argument is not read there).  vd_attention_short_path(d) says whether d takes that path;
  * vd_attention_set_short(0) (or env VDIFF_ATTN_SHORT=0) routes such shapes to the flash
  * kernels instead (A/B and test hook; returns the previous setting).  No reference
  * counterpart: the reference materialises T x T scores (unet.py:361-365 per regrouped
