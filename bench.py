@@ -73,7 +73,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=2,
                     help="frames of the bounded CPU-baseline clip (config-2 model, "
                          "spatial_temporal)")
-    ap.add_argument("--only", choices=["train", "ddim", "vivit", "all"], default="all")
+    ap.add_argument("--only", choices=["train", "ddim", "ddim_st", "vivit", "all"], default="all",
+                    help="ddim_st: only the spatial_temporal DDIM leg (profiling)")
     ap.add_argument("--ddim-eager", action="store_true",
                     help="DDIM legs without the HIP-graph replay (A/B)")
     ap.add_argument("--vivit-steps", type=int, default=20,
@@ -539,6 +540,57 @@ def st_leg(args, rank, world, device):
     return out
 
 
+def ddim_st_leg(args, world, device, init_state, sampler, clip, kd):
+    """The north-star forward in the factorised mode (VERDICT r05 missing #1): one DDIM
+    denoising step (UNet3D forward at 128x128x16 in spatial_temporal mode, SURVEY D1 -- per-frame
+    spatial attention over H*W tokens + per-pixel temporal attention over T tokens -- plus the
+    DDIM update) replayed as the product's HIP graph, the same weights and inputs as the joint
+    `ddim` leg.  frac = the forward's algorithmic FLOP (vdiff.flops.unet_forward_work) per second
+    / the bf16 MFMA peak."""
+    import copy as _copy
+    from vdiff import ops
+    from vdiff.flops import unet_forward_work
+    a2 = _copy.copy(args)
+    a2.mode = "spatial_temporal"
+    model = build_model(a2, device)
+    with torch.no_grad():
+        # the shared weights of the joint leg; the temporal blocks (spatial_temporal only)
+        # keep build_model's benchmark init
+        miss = model.load_state_dict(init_state, strict=False)
+    assert not miss.unexpected_keys and all(".temporal_" in k for k in miss.missing_keys), miss
+    model.eval()
+    work = unet_forward_work(model, (1, 195, args.frames, args.size, args.size))
+    with torch.no_grad(), ops.frozen_weights():
+        feats = model.encode_audio(clip.audio)
+        xt = torch.randn_like(clip.x0)
+        step = ddim_stepper(args, model, sampler, clip.cond, feats, xt)
+        step(0)  # warm-up (and, graphed, the capture)
+        barrier_sync(world)
+        t0 = time.perf_counter()
+        for i in range(1, 1 + kd):
+            step(i)
+        barrier_sync(world)
+        el = max_over_ranks(time.perf_counter() - t0, world, device)
+        del step
+    tf = work.total / (el / kd) / 1e12
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    out = {"metric": "DDIM steps/sec, 128x128x16 UNet3D, spatial_temporal attention (SURVEY D1)",
+           "value": round(world * kd / el, 4), "unit": "steps/s", "steps_timed": kd,
+           "ms_per_step": round(el / kd * 1e3, 3),
+           "fwd_tflop": round(work.total / 1e12, 3),
+           "fwd_tflop_conv": round(work.conv / 1e12, 3),
+           "fwd_tflop_attn": round(work.attn / 1e12, 3),
+           "model_tflops_per_gpu": round(tf, 1), "peak": peak, "frac": round(tf / peak, 4),
+           "hip_graph": not args.ddim_eager,
+           "note": "frac = forward algorithmic FLOP / (ms per DDIM step) / peak; the step also "
+                   "runs the DDIM update (HBM-bound, a few microseconds)"}
+    log(f"ddim_st: {out['ms_per_step']} ms/step, {out['model_tflops_per_gpu']} TFLOP/s, "
+        f"frac {out['frac']}")
+    del model
+    torch.cuda.empty_cache()
+    return out
+
+
 def _num(x, nd=4):
     """A float for the JSON line: None when not finite (NaN / Infinity are not JSON)."""
     x = float(x)
@@ -746,6 +798,14 @@ def main():
         del trainer, bank
         torch.cuda.empty_cache()
 
+    if args.only == "ddim_st":
+        kd = args.ddim_steps or args.steps
+        sampler = DDIMSampler(LinearNoiseSchedulerV2(500, 0.00005, 0.015), steps=50)
+        clip = synthetic_clip(1, args.frames, args.size, 500, device, seed=100 + rank)
+        result["ddim_st"] = ddim_st_leg(args, world, device, init_state, sampler, clip, kd)
+        result.update(value=result["ddim_st"]["value"], unit="steps/s",
+                      ms_per_step=result["ddim_st"]["ms_per_step"])
+
     if args.only in ("ddim", "all"):
         with torch.no_grad():
             model.load_state_dict(init_state)
@@ -771,6 +831,13 @@ def main():
                 "model_tflops_per_gpu": round(work.total / (el / kd) / 1e12, 1)}
         result["ddim"] = ddim
         log(f"ddim: {ddim['ms_per_step']} ms/step, {ddim['value']} steps/s")
+        if args.st_steps != 0 and args.mode == "joint":
+            try:  # an auxiliary leg: never let it take the headline numbers down
+                result["ddim_st"] = ddim_st_leg(args, world, device, init_state, sampler, clip,
+                                                kd)
+            except Exception as e:
+                log(f"ddim_st leg failed: {type(e).__name__}: {e}")
+                result["ddim_st"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
         if args.c4_steps > 0:
             # BASELINE config 4: 256x256x25-frame UNet3D, 50-step DDIM (test.py path), one clip
             # per GPU; the same weights (the UNet is size-agnostic), audio encoded once

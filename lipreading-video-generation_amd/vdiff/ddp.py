@@ -17,6 +17,8 @@ from __future__ import annotations
 
 import os
 
+import weakref
+
 import torch
 import torch.distributed as dist
 
@@ -113,13 +115,22 @@ class GradBucketer:
         self.bucket_of = {}
         self.index = {}  # param -> position in self.used
         self.views = []  # (param, its gradient view into the bucket buffer)
+        # the hooks hold the bucketer weakly: a bound method would make a parameter -> hook ->
+        # bucketer -> parameter cycle, so a dropped bucketer (its gradient buffers and pinned
+        # flags) would wait for the cyclic collector instead of being released at once
+        ref = weakref.ref(self)
+
+        def hook(p):
+            me = ref()
+            if me is not None:
+                me._hook(p)
         for b in self.buckets:
             for p in b.params:
                 self.bucket_of[p] = b
                 self.index[p] = len(self.views)
                 self.views.append((p, p.grad))
                 if self.world > 1:
-                    p.register_post_accumulate_grad_hook(self._hook)
+                    p.register_post_accumulate_grad_hook(hook)
         self.used = [0] * len(self.views)  # this rank: did the parameter get a gradient
         self.unused_local: list[int] = []
         if self.buckets:

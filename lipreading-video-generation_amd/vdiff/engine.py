@@ -14,6 +14,7 @@ import contextlib
 import math
 import os
 import warnings
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -189,10 +190,18 @@ class TrainStepGraph:
     reset to None."""
 
     def __init__(self, trainer, warmup=2):
-        self.tr = trainer
+        # a weak reference: Trainer -> TrainStepGraph -> Trainer would be a reference cycle,
+        # so a dropped trainer's CUDAGraph would be destroyed by the cyclic collector -- which
+        # may run inside a later capture, where ~CUDAGraph's device synchronisation is refused
+        # and the process aborts (round 5; DESIGN section 9.3, hipgraph.capture)
+        self._tr = weakref.ref(trainer)
         self.warmup = int(warmup)
         self.g = None
         self.steps = 0
+
+    @property
+    def tr(self):
+        return self._tr()
 
     def step(self, clip: Clip) -> torch.Tensor:
         tr = self.tr
@@ -301,6 +310,10 @@ def sample_ddim(model, sampler, cond, audio, shape, generator=None, callback=Non
         return _sample_ddim(model, sampler, cond, audio, shape, generator, callback)
 
 
+class GraphUnsafe(RuntimeError):
+    """A captured graph holds a node type that is not safe to replay (a memset node)."""
+
+
 class DDIMGraph:
     """One deterministic DDIM denoising step -- UNet forward + vd_ddim_step -- captured once
     as a HIP graph and replayed per step (no per-kernel launch gaps, no host work per
@@ -331,7 +344,9 @@ class DDIMGraph:
         self.xt.copy_(xp.view_as(self.xt))
         return x0
 
-    def _capture(self):
+    def capture(self):
+        """Warm up eagerly and capture one step (step() does this on first use).  Raises
+        GraphUnsafe if the captured step holds a memset node."""
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream(device=self.xt.device)
         side.wait_stream(cur)
@@ -340,16 +355,27 @@ class DDIMGraph:
             self._body()
             self.xt.copy_(keep)
         cur.wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)  # node list kept (node_types)
         with hipgraph.capture(self.graph):
             self.x0 = self._body()
+        self.graph.instantiate()
+        types = self.node_types()
+        if types.get("memset", 0):
+            # a memset node replayed with eager work between replays is
+            # where a captured reduction went stale on this HIP runtime; sample() steps
+            # eagerly instead of trusting such a graph
+            raise GraphUnsafe(f"DDIMGraph: captured step holds memset nodes {types}")
+
+    def node_types(self):
+        """{node type: count} of the captured step (vdiff.hipgraph; memset nodes must be 0)."""
+        return hipgraph.node_counts(self.graph)
 
     def step(self, i):
         """Denoise from sampler.timesteps[i]; returns (x_prev, x0) (static buffers)."""
         self.t.copy_(self.t_all[i])
         self.tp.copy_(self.tp_all[i])
         if self.graph is None:
-            self._capture()
+            self.capture()
         self.graph.replay()
         return self.xt, self.x0.view_as(self.xt)
 
@@ -367,11 +393,17 @@ def _sample_ddim(model, sampler, cond, audio, shape, generator, callback):
     x0 = None
     if _use_graph(device, sampler):
         g = DDIMGraph(model, sampler, cond, feats, xt)
-        for i in range(sampler.steps):
-            xt, x0 = g.step(i)
-            if callback is not None:  # the graph's static buffers: the next replay rewrites them
-                callback(i, xt.clone(), x0.clone())
-        return xt.clone(), x0.clone()
+        try:
+            g.capture()
+        except GraphUnsafe as e:
+            warnings.warn(f"{e}; sampling eagerly")
+            g = None
+        if g is not None:
+            for i in range(sampler.steps):
+                xt, x0 = g.step(i)
+                if callback is not None:  # the graph's static buffers: the next replay rewrites them
+                    callback(i, xt.clone(), x0.clone())
+            return xt.clone(), x0.clone()
     for i in range(sampler.steps):
         t = torch.full((shape[0],), int(sampler.timesteps[i]), dtype=torch.int64, device=device)
         eps = model(xt, cond, feats, t)

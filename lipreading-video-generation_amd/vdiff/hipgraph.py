@@ -57,6 +57,15 @@ def graph_nodes(raw_graph):
     return out
 
 
+def node_counts(graph):
+    """{node type: count} of a torch.cuda.CUDAGraph captured with keep_graph=True."""
+    nodes = graph_nodes(graph.raw_cuda_graph())
+    out = {}
+    for n in nodes:
+        out[n["type"]] = out.get(n["type"], 0) + 1
+    return out
+
+
 def read_i32(dev_ptr, count=1):
     """count int32 values at a device address (synchronous hipMemcpy, device -> host)."""
     buf = (ctypes.c_int32 * count)()
@@ -67,11 +76,18 @@ def read_i32(dev_ptr, count=1):
 
 @contextlib.contextmanager
 def capture(graph, **kw):
-    """torch.cuda.graph(graph, **kw) with Python's garbage collector off for the capture.
-    torch collects once before capturing, but a collection triggered by allocations DURING
-    the capture runs finalizers on the capturing thread, and a finalizer that calls a HIP API
-    a capture forbids aborts the process (seen once in the -m gpu suite, round 5: 'Fatal
-    Python error: Aborted' under 'Garbage-collecting' inside TrainStepGraph._capture)."""
+    """torch.cuda.graph(graph, **kw) with Python's cyclic garbage collector run BEFORE the
+    capture and kept off DURING it.
+
+    torch.cuda.graph does not collect before capture_begin (force_cudagraph_gc is False), so
+    reference cycles left by earlier work are collected by whichever allocation crosses the
+    collector's threshold -- inside the capture, on the capturing thread.  A dead
+    torch.cuda.CUDAGraph in such a cycle is then destroyed inside the capture: ~CUDAGraph's
+    device synchronisation (HIPGraph.cpp:324, ROCm builds) returns
+    hipErrorStreamCaptureUnsupported, AT_CUDA_CHECK throws in a destructor and std::terminate
+    aborts the process -- round 5's 'Fatal Python error: Aborted' under 'Garbage-collecting'
+    inside TrainStepGraph._capture, where an earlier test's Trainer <-> TrainStepGraph cycle
+    held the graph (tools/capture_finalizer_probe.py)."""
     enabled = gc.isenabled()
     gc.collect()
     gc.disable()

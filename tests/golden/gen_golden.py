@@ -296,7 +296,7 @@ def gen_train_step():
         ["audio_transformer.transform.0.weight", "audio_transformer.transform.0.bias",
          "cond_conv_in.weight"]
     before = [p.detach().clone() for p in params]
-    opt = torch.optim.Adam(params, 1e-2)  # train.py:102
+    opt = torch.optim.Adam(params, lr)  # train.py:102 (lr=1e-2)
     opt.zero_grad()
     xt = sched.add_noise(x0, eps, t)
     a = F.relu(lin(feat)).reshape(1, T, 16).permute(0, 2, 1).reshape(1, 16, T, 1, 1)
@@ -321,14 +321,16 @@ def gen_train_step():
 
 
 # ------------------------------------------------------------------ five train steps
-def gen_train_steps5():
+def gen_train_steps5(lr=1e-2, name="train_steps5_tiny3d.npz"):
     """Five consecutive steps of the reference training loop (train.py:107-134) on BASELINE
     config 1's shape: ONE torch.optim.Adam(lr=1e-2) over the imported reference UNetModel plus
     the restated conditioning (as gen_train_step), a new seeded batch, noise and timestep per
     step.  Saves every step's loss, the step-1 and step-5 gradients and the five-step
     parameter change of selected parameters: the pin of the product Trainer beyond one step
     (the product packs its conv operands per call in step 1 and in one
-    batched launch from step 2 on)."""
+    batched launch from step 2 on).  lr: train.py:102's 1e-2 (the default fixture), or 1e-4,
+    the rate bench.py's headline trains at (train_steps5_tiny3d_lr1e-4.npz, VERDICT r05
+    item 4)."""
     m = ref_unet.UNetModel(image_size=64, **TINY3D)
     m.train()
     load_init(m, 1234)
@@ -345,7 +347,7 @@ def gen_train_steps5():
         ["audio_transformer.transform.0.weight", "audio_transformer.transform.0.bias",
          "cond_conv_in.weight"]
     before = [p.detach().clone() for p in params]
-    opt = torch.optim.Adam(params, 1e-2)  # train.py:102
+    opt = torch.optim.Adam(params, lr)  # train.py:102 (lr=1e-2)
     sel = ("input_blocks.0.0.weight", "out.2.weight", "input_blocks.3.1.qkv.weight",
            "input_blocks.3.1.proj_out.weight", "middle_block.0.in_layers.0.weight",
            "output_blocks.0.0.skip_connection.weight", "time_embed.0.weight",
@@ -373,7 +375,8 @@ def gen_train_steps5():
     for n, p, b in zip(names, params, before):
         if n in sel:
             out["delta5_" + n] = p.detach() - b
-    save("train_steps5_tiny3d.npz", **out)
+    out["lr"] = torch.tensor(lr)
+    save(name, **out)
 
 
 # ------------------------------------------------------------------ sampling trajectories
@@ -481,5 +484,7 @@ if __name__ == "__main__":
         gen_train_step()
     if "train_steps5" in which:
         gen_train_steps5()
+    if "train_steps5_lr1e-4" in which:
+        gen_train_steps5(1e-4, "train_steps5_tiny3d_lr1e-4.npz")
     if "trajectory" in which:
         gen_trajectory()

@@ -49,10 +49,19 @@ def _worker(rank, world, port, out):
         bk.finish()
         if step == 0:
             bk.zero_grad()
+    # the gradient hooks hold the bucketer weakly: dropping it frees it (and its pinned flag
+    # buffer) at once, without the cyclic collector
+    import gc
+    import weakref
+    nb, ref = len(bk.buckets), weakref.ref(bk)
+    gc.disable()
+    del bk
+    freed = ref() is None
+    gc.enable()
     if rank == 0:
         # numpy arrays travel by value: a tensor would travel as a shared-memory fd whose
         # sharer thread dies with this process, racing the parent's get()
-        out.put([p.grad.detach().numpy().copy() for p in m.parameters()] + [len(bk.buckets)])
+        out.put([p.grad.detach().numpy().copy() for p in m.parameters()] + [freed, nb])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,12 +75,13 @@ def test_bucketed_allreduce_matches_single_process():
     for p in procs:
         p.start()
     got = q.get(timeout=240)
-    got = [torch.from_numpy(a) for a in got[:-1]] + [torch.tensor(got[-1])]
+    freed, nb = got[-2], int(got[-1])
+    got = [torch.from_numpy(a) for a in got[:-2]]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    nb = int(got.pop())
     assert nb >= 2
+    assert freed, "GradBucketer was kept alive by a reference cycle"
     m = _model()
     x, y = _data()
     torch.nn.functional.mse_loss(m(x), y).backward()
@@ -119,10 +129,19 @@ def _skip_worker(rank, world, port, out):
         bk.finish()
         if step == 0:
             bk.zero_grad()
+    # the gradient hooks hold the bucketer weakly: dropping it frees it (and its pinned flag
+    # buffer) at once, without the cyclic collector
+    import gc
+    import weakref
+    nb, ref = len(bk.buckets), weakref.ref(bk)
+    gc.disable()
+    del bk
+    freed = ref() is None
+    gc.enable()
     if rank == 0:
         # numpy arrays travel by value: a tensor would travel as a shared-memory fd whose
         # sharer thread dies with this process, racing the parent's get()
-        out.put([p.grad.detach().numpy().copy() for p in m.parameters()] + [len(bk.buckets)])
+        out.put([p.grad.detach().numpy().copy() for p in m.parameters()] + [freed, nb])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -138,11 +157,12 @@ def test_bucket_order_survives_rank_dependent_unused_params():
     for p in procs:
         p.start()
     got = q.get(timeout=240)
-    got = [torch.from_numpy(a) for a in got[:-1]] + [torch.tensor(got[-1])]
+    freed, nb = got[-2], int(got[-1])
+    got = [torch.from_numpy(a) for a in got[:-2]]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert int(got.pop()) >= 4
+    assert nb >= 4 and freed
     grads = []
     for r in range(world):
         m = _Skippy()

@@ -327,7 +327,7 @@ def test_trainer_step_matches_reference_adam_step():
         assert adam_delta_close(d, g["delta_" + k], g["grad_" + k]) < 1e-6, k
 
 
-def _five_steps(bf16):
+def _five_steps(bf16, lr=1e-2, fixture="train_steps5_tiny3d.npz"):
     """Five steps of the DEFAULT Trainer (conv operands packed per call in step 1, by the
     batched launch from step 2 on; fused Adam lr 1e-2 whose moments carry over) on the
     inputs of the five-step reference fixture (train.py:107-134,
@@ -337,7 +337,9 @@ def _five_steps(bf16):
     from vdiff.engine import Clip, Trainer
     from vdiff.schedulers import LinearNoiseScheduler
     from vdiff.unet_audio import UNetAudio
-    g = golden("train_steps5_tiny3d.npz")
+    g = golden(fixture)
+    if "lr" in g:
+        assert abs(float(g["lr"]) - lr) <= 1e-6 * lr, (float(g["lr"]), lr)  # stored fp32
     m = UNetAudio(image_size=64, in_channels=3, model_channels=32, out_channels=3,
                   num_res_blocks=1, attention_resolutions=(2,), channel_mult=(1, 2), dims=3,
                   audio_feature_dim=64, projected_audio_dim=16, im_cond_output_ch=16,
@@ -351,7 +353,7 @@ def _five_steps(bf16):
         m.convert_to_fp16()   # the bench's mode: bf16 activations, fp32 master weights
     m = m.to(dev)
     before = {k: v.detach().clone() for k, v in m.named_parameters()}
-    tr = Trainer(m, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-2)
+    tr = Trainer(m, LinearNoiseScheduler(100, 0.00085, 0.012), lr=lr)
     assert tr.packs.__class__.__name__ == "step_packed_weights"  # the default path
     grads = {}
     step = [0]
@@ -382,7 +384,7 @@ def _five_steps(bf16):
              "grad5": max(v[1] for k, v in rep.items() if k != "loss"),
              "delta5": max(v[2] for k, v in rep.items() if k != "loss")}
     record_metric(test="trainer_five_steps_vs_reference", mode="bf16" if bf16 else "fp32",
-                  loss_max_rel=err_l, worst=worst,
+                  lr=lr, loss_max_rel=err_l, worst=worst,
                   per_param={k: v for k, v in rep.items() if k != "loss"})
     print("five-step parity", "bf16" if bf16 else "fp32", worst, rep)
     return rep, worst
@@ -459,6 +461,32 @@ def test_trainer_five_steps_bf16_match_reference():
     for k in ("grad1", "grad5", "delta5"):
         assert worst[k] <= auto[k], (k, worst, auto)
     assert rep["loss"] <= auto["loss"], (rep["loss"], auto)
+
+
+def test_trainer_five_steps_bf16_at_bench_lr_match_reference():
+    """the bf16 Trainer -- the path bench.py times -- at bench.py's Adam lr
+    1e-4 against five fp32 steps of the imported reference at that lr
+    (train_steps5_tiny3d_lr1e-4.npz).  At this lr the trajectories do not separate after step
+    1 (every Adam step is 1e-4, not 1e-2), so every figure constrains the kernels.  Measured
+    round 6 (profiles/r06_parity_metrics.jsonl): losses 2.3e-4, step-1 gradients 1.3e-2,
+    step-5 gradients 1.5e-2, five-step change 5.9e-2.  Bars about 3x those, capped at the bars
+    VERDICT r05 set (3e-2 / 1e-1 / 1e-1): 1e-3, 4e-2, 5e-2, 1e-1.  The five-step change sits
+    above the gradients because Adam's g / (sqrt(v) + eps) turns bf16-level differences on
+    near-zero gradient components into steps of up to lr (oracle.fixtures.adam_delta_close)."""
+    rep, worst = _five_steps(bf16=True, lr=1e-4, fixture="train_steps5_tiny3d_lr1e-4.npz")
+    assert rep["loss"] < 1e-3, rep
+    assert worst["grad1"] < 4e-2 and worst["grad5"] < 5e-2, (worst, rep)
+    assert worst["delta5"] < 1e-1, (worst, rep)
+
+
+def test_trainer_five_steps_fp32_at_bench_lr_match_reference():
+    """The fp32 parity-mode Trainer against the same lr-1e-4 fixture: the bars of the lr-1e-2
+    fp32 pin (the GPU's fp32 reductions differ from the CPU's in order only; measured round 6:
+    losses 9.4e-8, step-1 / step-5 gradients 1.9e-6 / 5.0e-6, five-step change 1.8e-5)."""
+    rep, worst = _five_steps(bf16=False, lr=1e-4, fixture="train_steps5_tiny3d_lr1e-4.npz")
+    assert rep["loss"] < 1e-4, rep
+    assert worst["grad1"] < 1e-4 and worst["grad5"] < 1e-3, rep
+    assert worst["delta5"] < 5e-4, rep
 
 
 def _pack_runs(m, modes, lr, steps=3):

@@ -355,3 +355,64 @@ def test_capture_runs_without_garbage_collection():
     g.replay()
     torch.cuda.synchronize()
     assert float(x[0]) == 2.0
+
+
+def test_capture_completes_with_a_dead_graph_in_a_cycle():
+    """the object behind the round-5 abort -- a captured, replayed
+    torch.cuda.CUDAGraph stranded in an unreachable reference cycle (as the Trainer <->
+    TrainStepGraph cycle of an earlier test held one).  Destroyed by the cyclic collector inside
+    a capture, ~CUDAGraph's device synchronisation (HIPGraph.cpp:324, ROCm builds) returns
+    hipErrorStreamCaptureUnsupported, AT_CUDA_CHECK throws in a destructor and std::terminate
+    aborts (tools/capture_finalizer_probe.py, profiles/r06_capture_probe.jsonl).
+    hipgraph.capture collects it before capture_begin and keeps the collector off while
+    allocation-heavy host code runs inside."""
+    import gc
+    import weakref
+    from vdiff import hipgraph
+
+    class Holder:
+        pass
+    x = torch.zeros(1024, device=dev)
+    h = Holder()
+    h.me = h
+    h.graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(h.graph):
+        x.add_(1.0)
+    h.graph.replay()
+    torch.cuda.synchronize()
+    ref = weakref.ref(h)
+    del h
+    assert ref() is not None and gc.isenabled()
+    g = torch.cuda.CUDAGraph()
+    seen = []
+    with hipgraph.capture(g, capture_error_mode="thread_local"):
+        seen.append(ref() is None)
+        junk = [[i] for i in range(100000)]  # container allocations past gc thresholds
+        x.add_(1.0)
+    del junk
+    g.replay()
+    torch.cuda.synchronize()
+    assert seen == [True] and float(x[0]) == 2.0
+
+
+def test_dropped_graph_trainer_is_freed_without_the_collector():
+    """Trainer <-> TrainStepGraph hold each other weakly in one direction, so a dropped
+    graph trainer (its captured graph, memory pool and static buffers) is released at once by
+    reference counting, never by a collection that could fall inside a later capture."""
+    import gc
+    import weakref
+    from vdiff.engine import Trainer
+    from vdiff.schedulers import LinearNoiseScheduler
+    m = _model()
+    tr = Trainer(m, LinearNoiseScheduler(100, 0.00085, 0.012), lr=1e-3, graph=True)
+    c = _clip(0, False)
+    for _ in range(3):
+        tr.step(c)
+    assert tr.graph.g is not None
+    refs = [weakref.ref(tr), weakref.ref(tr.graph), weakref.ref(tr.graph.g)]
+    gc.disable()
+    try:
+        del tr
+        assert all(r() is None for r in refs)
+    finally:
+        gc.enable()

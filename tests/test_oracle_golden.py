@@ -1,5 +1,6 @@
 """Pin the oracle (CPU restatement) to the golden vectors made by importing the
 reference (tests/golden/gen_golden.py).  CPU only."""
+import pytest
 import torch
 import torch.nn.functional as F
 
@@ -195,21 +196,24 @@ def test_one_adam_train_step():
         assert adam_delta_close(deltas[k], g["delta_" + k], g["grad_" + k]) < 1e-6, k
 
 
-def test_five_adam_train_steps():
+@pytest.mark.parametrize("lr,fixture", [(1e-2, "train_steps5_tiny3d.npz"),
+                                         (1e-4, "train_steps5_tiny3d_lr1e-4.npz")])
+def test_five_adam_train_steps(lr, fixture):
     """the oracle's training loop (one Adam over five steps, a new seeded
     batch / noise / t per step) against the reference's (train.py:107-134, imported by
     tests/golden/gen_golden.py gen_train_steps5): losses, step-1 / step-5 gradients and the
-    five-step parameter change."""
+    five-step parameter change; at train.py:102's lr 1e-2 and at bench.py's 1e-4 (VERDICT r05
+    item 4)."""
     from oracle.fixtures import TRAIN5_T, train5_inputs
     from oracle.train import train_steps
-    g = golden("train_steps5_tiny3d.npz")
+    g = golden(fixture)
     assert tuple(g["t"].tolist()) == TRAIN5_T
     plan = build_plan(**TINY3D)
     P = init_params(param_shapes(plan), 1234)
     P.update(init_params(audio_param_shapes(64, 16, im_cond_output_ch=16), 77))
     P0 = {k: v.clone() for k, v in P.items()}
     batches = [train5_inputs(k) + (torch.tensor([t]),) for k, t in enumerate(TRAIN5_T)]
-    losses, kept = train_steps(P, plan, batches, 16, keep_grads=(0, 4))
+    losses, kept = train_steps(P, plan, batches, 16, lr=lr, keep_grads=(0, 4))
     close(losses, g["losses"], atol=1e-6, rtol=1e-5)
     names = [k[len("delta5_"):] for k in g if k.startswith("delta5_")]
     assert len(names) == 9

@@ -1,6 +1,8 @@
 """Per-step kernel time by category from a rocprofv3 --kernel-trace database of a bench run:
 steps are cut at each q_sample launch (one per train step); prints the categories of the
-last steps (the timed ones) in ms per step.   python tools/prof_steps.py run_results.db"""
+last steps (the timed ones) in ms per step.   python tools/prof_steps.py run_results.db [cut]
+cut: a kernel-name substring that starts each step (default QSample; ddim_kernel for DDIM).
+Also prints the per-kernel table (name, launches, ms) of the last step."""
 import sqlite3
 import sys
 
@@ -36,8 +38,9 @@ def cat(n):
 c = sqlite3.connect(sys.argv[1])
 ks = [(short(n), s, e) for n, s, e in
       c.execute("select name, start, end from kernels order by start")]
-cuts = [s for n, s, e in ks if "QSample" in n]
-print(f"{len(cuts)} steps (q_sample launches)")
+CUT = sys.argv[2] if len(sys.argv) > 2 else "QSample"
+cuts = [s for n, s, e in ks if CUT in n]
+print(f"{len(cuts)} steps ({CUT} launches)")
 for i in range(max(0, len(cuts) - 4), len(cuts)):
     lo, hi = cuts[i], cuts[i + 1] if i + 1 < len(cuts) else float("inf")
     agg, wall0, wall1 = {}, None, None
@@ -50,6 +53,18 @@ for i in range(max(0, len(cuts) - 4), len(cuts)):
     print(f"step {i}: kernels {tot:.1f} ms, first->last {(wall1 - wall0) / 1e6:.1f} ms")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1]):
         print(f"   {k:38s} {v:8.2f}")
+
+# the last complete step's kernels by name
+lo, hi = cuts[-2], cuts[-1]
+per = {}
+for n, s, e in ks:
+    if lo <= s < hi:
+        r = per.setdefault(n[:90], [0, 0.0])
+        r[0] += 1
+        r[1] += (e - s) / 1e6
+print("last complete step, per kernel (launches, ms):")
+for n, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:40]:
+    print(f"   {t:8.3f} ms  x{c:<4d} {n}")
 
 # idle gaps of the last step: the 12 largest, with the kernels on either side
 lo = cuts[-1]
