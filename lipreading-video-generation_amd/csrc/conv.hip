@@ -1304,51 +1304,52 @@ void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, c
 // The gathered-tile kernel above DMAs every tap's A tile separately: for 64 output channels
 // that is 4 of the 5 LDS-DMA pieces a wave issues per 32 MFMAs (and ~60 cycles of issue each,
 // MI355X_MICROARCH.md), so the 64-channel convs are DMA-issue bound.  Here a workgroup owns an
-// output tile of 2 x 4 x 16 pixels (t, h, w) x 64 channels; per 64-channel step the input
-// halo of the tile (4 x 6 x 18 pixels, 54 KiB) lands in LDS once, and all 27 taps read their
-// A fragments from it at shifted pixel offsets (16 consecutive w per fragment row group: with
-// the chunk swizzle of ig_off the 16 lanes hit 16 distinct bank quads for any shift).  Only
-// each tap's 64 x 64 weight slice (8 KiB) streams, through a 3-stage ring.  Pieces per wave
-// per tap: 2 (weights) + 14 / 27 (halo).  Transposed (bwd-data, stride 1): the same halo with
-// the tap offsets mirrored (source pixel = out + 1 - tap).  Needs W % 16 == 0; partial t / h
-// tiles are masked (zero halo rows, skipped stores).
+// output tile of 2 x 4 x 16 pixels (t, h, w) x 64 channels; per KS-channel step the input halo
+// of the tile (4 x 6 x 18 pixels) lands in LDS once, and all 27 taps read their A fragments
+// from it at shifted pixel offsets.  Only each tap's 64 x KS weight slice streams, through a
+// 3-stage ring (one workgroup barrier per tap).  Transposed (bwd-data, stride 1): the same halo
+// with the tap offsets mirrored (source pixel = out + 1 - tap).  Needs W % 16 == 0; partial
+// t / h tiles are masked (zero halo rows, skipped stores).
 constexpr int kHoT = 2, kHoH = 4, kHoW = 16;                    // output tile
 constexpr int kHaT = kHoT + 2, kHaH = kHoH + 2, kHaW = kHoW + 2;  // input halo
 constexpr int kHaP = kHaT * kHaH * kHaW;                         // 432 pixels = 54 pieces
 // KS channels per step: 64 (128-B LDS rows, 80 KiB per workgroup, two per CU) or 32 (64-B
-// rows, 40 KiB, four per CU); weight ring stages NSTB (prefetch distance NSTB - 1):
-// VDIFF_CONV_HALO_KS forces the channel step (A/B).
+// rows, 40 KiB, four per CU); weight ring stages NSTB (prefetch distance NSTB - 1).
 template <int NSTB, int KS>
 constexpr size_t halo_lds() { return (size_t)(kHaP + NSTB * 64) * 2 * KS + 1024; }  // + junk
 static_assert(kHaP % 16 == 0, "whole halo pieces");
-// element offset of 16-B chunk c of row r: 128-B rows as ig_off, 64-B rows with the chunk
-// XOR (r >> 2) & 3 -- 16 consecutive rows at one chunk then cover all 16 bank quads
+// Round 6: every tap unrolled.  The rolled tap loop spent ~35 SALU and ~16 VALU instructions
+// per tap deriving (dt, dh, dw) by division, the ring stage and the fragment addresses
+// (SQ_INSTS_SALU 2011 per wave for 432 MFMAs, 64->64 at 16x128x128), all on the wave's path
+// between two barriers.  Here the 27 taps are unrolled, so the tap offsets and ring stages are
+// immediates.  The halo swizzle is keyed on the pixel's column w inside its halo line (c ^ (w &
+// 6) for 128-B rows, c ^ ((w >> 1) & 2) for 64-B rows), so a fragment read is a per-lane base
+// chosen by dw (3 per fragment row) plus a compile-time offset.  ds_read_b128 serves lanes in
+// groups of 16 ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} and the same + 32): one LDS cycle
+// mixes rows r, r + 12 (even fq) with r + 4, r + 8 (odd fq); these XOR terms give those lanes
+// 16 distinct bank quads for any start row (searched exhaustively; the round-5 (r >> 2) & 3 /
+// (r >> 1) & 7 terms were 2-way conflicted: SQ_LDS_BANK_CONFLICT was 47 % of the LDS cycles).
+// A fragments of tap t + 1 are read during tap t (the halo is stable within a channel step;
+// only the weight ring needs the per-tap barrier).
 template <int KS>
-__device__ __forceinline__ int ha_off(int r, int c) {
-  if constexpr (KS == 64) return ig_off(r, c);
-  else return r * 32 + ((c ^ ((r >> 2) & 3)) << 3);
-}
-template <int KS>
-__device__ __forceinline__ int ha_swz(int r) {
-  if constexpr (KS == 64) return (r >> 1) & 7;
-  else return (r >> 2) & 3;
+__device__ __forceinline__ int h2_swz(int w) {
+  if constexpr (KS == 64) return w & 6;
+  else return (w >> 1) & 2;
 }
 
-template <bool TR, int NSTB, int NW, int KS>
-__global__ __launch_bounds__(64 * NW, NSTB <= 3 ? (KS == 32 ? 4 : 2) : 1) void halo_conv_kernel(
+template <bool TR, int KS>
+__global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
     GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
     bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
     const bf16_t* __restrict__ residual) {
-  // NW waves: each owns NI = 8 / NW fragment rows (16 output pixels each) of the 128-pixel tile
+  constexpr int NW = 4, NSTB = 3, PD = NSTB - 1;
   constexpr int RB = 2 * KS, PPP = 1024 / RB, CPR = KS / 8;  // row bytes, rows per piece, chunks
   constexpr int HP = kHaP / PPP;                                // halo pieces
-  constexpr int BN = 64, NI = 8 / NW, NJ = 4, IB = BN / PPP / NW, TAPS = 27;
+  constexpr int BN = 64, NI = 8 / NW, NJ = 4, IB = BN / PPP / NW, TAPS = 27, NS = KS / 32;
   constexpr int HPW = (HP + NW - 1) / NW;                       // halo pieces per wave
   static_assert(IB >= 1, "one weight piece per wave at least");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const bf16_t* halo = reinterpret_cast<const bf16_t*>(smem);
   char* ring = smem + kHaP * RB;
-  constexpr int PD = NSTB - 1;
   char* junk = ring + NSTB * BN * RB;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1368,14 +1369,12 @@ __global__ __launch_bounds__(64 * NW, NSTB <= 3 ? (KS == 32 ? 4 : 2) : 1) void h
   const rsrc_t rs_a = make_rsrc(src, (uint32_t)((int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2));
   const rsrc_t rs_b = make_rsrc(wt, (uint32_t)((int64_t)g.N * g.K * 2));
 
-  // this wave's halo pieces q = wave + NW i: pixel p = PPP q + lane / CPR, physical chunk
-  // lane % CPR (it fetches the logical chunk that swizzles there)
   int h_off[HPW], h_c[HPW];
 #pragma unroll
   for (int i = 0; i < HPW; ++i) {
     const int q = wave + NW * i, p = PPP * q + lr;
-    const int c = pc ^ ha_swz<KS>(p);
     const int hw = p % kHaW, hh = (p / kHaW) % kHaH, ht = p / (kHaW * kHaH);
+    const int c = pc ^ h2_swz<KS>(hw);
     const int st = t0 - 1 + ht, sh = h0 - 1 + hh, sw = w0 - 1 + hw;
     const bool in = q < HP && (unsigned)st < (unsigned)g.sT &&
                     (unsigned)sh < (unsigned)g.sH && (unsigned)sw < (unsigned)g.sW;
@@ -1395,7 +1394,7 @@ __global__ __launch_bounds__(64 * NW, NSTB <= 3 ? (KS == 32 ? 4 : 2) : 1) void h
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int r = (wave * IB + i) * PPP + lr;
-    const int c = pc ^ ha_swz<KS>(r);
+    const int c = pc ^ h2_swz<KS>(r);
     b_c[i] = c * 8;
     const int n = n0 + r;
     b_off[i] = n < g.N ? n * g.K * 2 + c * 16 : -1;
@@ -1417,42 +1416,79 @@ __global__ __launch_bounds__(64 * NW, NSTB <= 3 ? (KS == 32 ? 4 : 2) : 1) void h
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
-  // the wave's two fragment rows: output rows (t_l, h_l) = blocks 2 wave, 2 wave + 1
-  int prow[NI];
+  // byte offsets (from smem) of this lane's A fragment rows at tap (0, 0, dw), sub-step s
+  int abase[NI][3][NS];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int rb = NI * wave + i, tl = rb / kHoH, hl = rb % kHoH;
-    prow[i] = (tl * kHaH + hl) * kHaW + fr;  // halo pixel of tap (0, 0, 0) (fwd orientation)
+    const int line = tl * kHaH + hl;
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int w = fr + d;
+        abase[i][d][s] = (line * kHaW + w) * RB + (((4 * s + fq) ^ h2_swz<KS>(w)) << 4);
+      }
   }
+  int bbase[NJ][NS];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int r = 16 * j + fr;
+      bbase[j][s] = kHaP * RB + r * RB + (((4 * s + fq) ^ h2_swz<KS>(r)) << 4);
+    }
 
   vm_drain();
   for (int cs = 0; cs < csteps; ++cs) {
-    __syncthreads();  // every wave is done with the previous step's halo and ring
+    lgk_wait_barrier();  // every wave's reads of the previous step's halo and ring returned
     issue_halo(cs);
 #pragma unroll
     for (int i = 0; i < PD; ++i) issue_b(cs, i);
+    // opaque per channel step: the compiler would otherwise hoist all 27 x NI per-tap fragment
+    // addresses out of the loop into VGPRs instead of folding the tap offsets into ds_read
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(abase[i][d][s]));
+    bf16x8 af[2][NI][NS];
+#pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
       // this tap's weights (and at tap 0 the halo) landed everywhere; stage tap-1 is free
-      vm_wait_barrier<(PD - 1) * IB>();
+      vm_lgk_wait_barrier<(PD - 1) * IB>();
       issue_b(cs, tap + PD);
-      const int a = tap / 9, bb = (tap / 3) % 3, cc = tap % 3;
-      const int dt = TR ? 2 - a : a, dh = TR ? 2 - bb : bb, dw = TR ? 2 - cc : cc;
-      const int shift = (dt * kHaH + dh) * kHaW + dw;
-      const bf16_t* Bs = reinterpret_cast<const bf16_t*>(ring + (tap % NSTB) * (BN * RB));
 #pragma unroll
-      for (int s = 0; s < KS / 32; ++s) {
-        bf16x8 af[NI], bfr[NJ];
+      for (int u = (tap == 0 ? 0 : 1); u < 2; ++u) {  // tap 0: its own A; every tap: the next
+        const int tp = tap + u;
+        if (tp >= TAPS) break;
+        const int a = tp / 9, bb = (tp / 3) % 3, cc = tp % 3;
+        const int dt = TR ? 2 - a : a, dh = TR ? 2 - bb : bb, dw = TR ? 2 - cc : cc;
+        const int lofs = (dt * kHaH + dh) * kHaW * RB;
+        if (u == 1 || tap == 0) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(halo + ha_off<KS>(prow[i] + shift, 4 * s + fq));
+          for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+              af[tp & 1][i][s] =
+                  *reinterpret_cast<const bf16x8*>(smem + abase[i][dw][s] + lofs);
+        }
+        if (tap == 0 && u == 0) continue;
+      }
+      const int so = (tap % NSTB) * (BN * RB);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        bf16x8 bfr[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ha_off<KS>(16 * j + fr, 4 * s + fq));
+          bfr[j] = *reinterpret_cast<const bf16x8*>(smem + bbase[j][s] + so);
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tap & 1][i][s], bfr[j],
+                                                                acc[i][j], 0, 0, 0);
       }
     }
   }
@@ -1509,58 +1545,51 @@ bool halo_ok(const GemmGeom& g) {
          g.pt == 1 && g.ph == 1 && g.pw == 1 && g.sT == g.dT && g.sH == g.dH && g.sW == g.dW &&
          g.dW % kHoW == 0;
 }
-// VDIFF_CONV_HALO: 0 never, 1 every eligible conv, 2 (default) where it measured faster
-// (halo_ks below; the list that follows is the 64-channel-step measurement).
-// Same-box per-shape A/B over the config-2 train step (profiles/r02_ab_conv_halo.txt): the
-// halo tile wins for N <= 64 (fwd 200->64 / 192->64 0.66x, 64->64 0.87x, bwd-data 64->64
-// 0.84x) and at the 32x32 level up to N = 256 (0.68-0.83x); with N >= 128 at 64x64 and
-// 128x128 the gathered 128 x 128 tiles keep the edge (1.0-1.1x): the halo kernel's N tile is
-// 64, so every 64 output channels re-load the halo.  Deeper weight rings (one workgroup per
-// CU) and 8 waves per workgroup measured slower (removed in round 5).
+// VDIFF_CONV_HALO / vd_conv_set_halo: 0 never (the gathered-tile kernel), 1 and 2 (default)
+// every eligible conv.  Round 6: with the conflict-free swizzle and the unrolled taps the halo
+// tile beats the gathered 128 x 128 tiles on every 3x3x3 shape of the step, fwd and bwd-data
+// (tools/conv3_bench.py, profiles/r06_conv3_ab.txt), so the round-2 per-shape selection (halo
+// only for N <= 64 and at the 32x32 level) is gone.
 std::atomic<int> g_halo_mode{[] {
   const char* e = getenv("VDIFF_CONV_HALO");
   return e ? atoi(e) : 2;
 }()};
 int conv_halo_mode() { return g_halo_mode.load(std::memory_order_relaxed); }
-// Channels per halo step for this conv, 0 = the gathered-tile kernel.  64-channel steps (two
-// workgroups per CU) win at the 32x32 level, 32-channel steps (four per CU) on the larger
-// levels; per-shape A/B in profiles/r02_ab_conv_halo_ks.txt.  N = output channels of the
-// GEMM (Co fwd, Ci bwd-data), sC = its reduction channels.
-int halo_ks(const GemmGeom& g, bool tr) {
-  const int m = conv_halo_mode();
-  if (m == 0 || !halo_ok(g)) return 0;
+// Channels per halo step for this conv, 0 = the gathered-tile kernel: 64-channel steps (80 KiB,
+// two workgroups per CU) at the 32x32 level and from 128 reduction channels on, 32-channel
+// steps (40 KiB, four per CU) otherwise; VDIFF_CONV_HALO_KS forces one (A/B).  sC = the GEMM's
+// reduction channels (Ci fwd, Co bwd-data).
+int halo_ks(const GemmGeom& g, bool /*tr*/) {
+  if (conv_halo_mode() == 0 || !halo_ok(g)) return 0;
   static const int force = [] {
     const char* e = getenv("VDIFF_CONV_HALO_KS");
     return e ? atoi(e) : 0;
   }();
-  const int natural = g.dW <= 32 ? 64 : 32;
-  if (m == 1) return force ? force : natural;
-  int ks = 0;
-  if (g.dW <= 32) ks = g.N <= 256 ? 64 : 0;
-  else if (!tr) ks = g.N <= 128 ? 32 : 0;
-  else ks = g.sC <= 64 ? 32 : (g.N <= 64 ? 64 : 0);
-  return ks && force ? force : ks;
+  if (force == 32 || force == 64) return force;
+  return (g.dW <= 32 || g.sC >= 128) ? 64 : 32;
 }
-template <bool TR, int NSTB, int NW, int KS = 64>
-void launch_halo_st(const GemmGeom& g, const void* src, const void* wt, void* dst,
-                    const float* bias, const float* ca, const void* res, hipStream_t st) {
+template <bool TR, int KS>
+void launch_halo_tile(const GemmGeom& g, const void* src, const void* wt, void* dst,
+                  const float* bias, const float* ca, const void* res, hipStream_t st) {
   const size_t lds_c = (size_t)128 * (64 + 4) * 4;
-  const size_t lds = halo_lds<NSTB, KS>() > lds_c ? halo_lds<NSTB, KS>() : lds_c;
-  auto kern = halo_conv_kernel<TR, NSTB, NW, KS>;
+  const size_t lds = halo_lds<3, KS>() > lds_c ? halo_lds<3, KS>() : lds_c;
+  auto kern = halo_conv_kernel<TR, KS>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int64_t tiles = (int64_t)g.B * vd_cdiv(g.dT, kHoT) * vd_cdiv(g.dH, kHoH) * (g.dW / kHoW);
   dim3 grid((unsigned)tiles, (unsigned)vd_cdiv(g.N, 64));
-  kern<<<grid, 64 * NW, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias,
-                                   ca, (const bf16_t*)res);
+  kern<<<grid, 256, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias, ca,
+                               (const bf16_t*)res);
 }
-// (8 waves per workgroup, a 5-stage weight ring and a 4-frame tile measured slower: DESIGN
-// section 4; removed)
+// (round 6, measured and removed: two taps per ring stage and barrier at three workgroups per CU
+// -- equal; a barrier-free form where each wave streams its own 16 weight rows for all 128
+// pixels -- 7 % slower, LDS-read bound at 9 fragment reads per 8 MFMAs.  Round 5: 8 waves per
+// workgroup, a 5-stage ring, a 4-frame tile.)
 template <bool TR>
 void launch_halo(const GemmGeom& g, int ks, const void* src, const void* wt, void* dst,
                  const float* bias, const float* ca, const void* res, hipStream_t st) {
-  if (ks == 32) launch_halo_st<TR, 3, 4, 32>(g, src, wt, dst, bias, ca, res, st);
-  else launch_halo_st<TR, 3, 4>(g, src, wt, dst, bias, ca, res, st);
+  if (ks == 32) launch_halo_tile<TR, 32>(g, src, wt, dst, bias, ca, res, st);
+  else launch_halo_tile<TR, 64>(g, src, wt, dst, bias, ca, res, st);
 }
 
 // ----------------------------------------------------------------- 1x1 convs: streaming GEMM

@@ -142,6 +142,16 @@ template <int N>
 __device__ __forceinline__ void vm_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
+// the same, after every LDS read of this wave has returned: the compiler may schedule the MFMAs
+// that consume earlier ds_reads (and so its own lgkmcnt waits) after an asm barrier, which would
+// leave a read of a stage in flight while another wave's DMA refills it
+template <int N>
+__device__ __forceinline__ void vm_lgk_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgk_wait_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 // compiler-visible (the waitcnt pass then knows every earlier global load has landed and
 // puts no waits of its own inside the ring loop); 0x0F70 = vmcnt(0), expcnt/lgkmcnt untouched
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }

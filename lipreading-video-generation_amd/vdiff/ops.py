@@ -1051,8 +1051,8 @@ class attention_config:
 
 class conv_halo:
     """Context manager selecting which 3x3x3 stride-1 bf16 convs take the halo-tile kernel
-    (vd_conv_set_halo): 0 none, 1 every eligible shape, 2 (default) where it measured faster.
-    Results agree up to fp32 summation order; used by tests and A/B benchmarks."""
+    (vd_conv_set_halo): 0 none (the gathered-tile kernel), 1 / 2 (default) every eligible
+    shape.  Results agree up to fp32 summation order; used by tests and A/B benchmarks."""
 
     def __init__(self, mode: int):
         if mode not in (0, 1, 2):

@@ -70,6 +70,43 @@ def test_conv_halo_hook_rejects_unknown():
         ops.conv_halo(5)
 
 
+# (Ci, Co, T, H = W): the train step's halo shapes at both channel steps, the one that showed a
+# nondeterministic result while the ring's stage reads could still be in flight across the
+# per-tap barrier (round 6: 192 -> 128 at 64x64, 64-channel steps), and ragged tiles
+DETERMINISM = [(64, 64, 16, 128), (192, 128, 16, 64), (256, 256, 16, 32), (200, 64, 4, 128),
+               (96, 80, 5, 32)]
+
+
+@pytest.mark.parametrize("shape", DETERMINISM)
+def test_halo_conv_is_deterministic(shape):
+    """Bit-identical outputs over repeated launches (fwd and bwd-data) at full train-step sizes:
+    every LDS read of a ring stage or halo returns before a barrier lets another wave's DMA refill
+    it (vm_lgk_wait_barrier), so no launch may differ from another."""
+    from vdiff import _lib, ops
+    Ci, Co, T, H = shape
+    g = torch.Generator(device=dev).manual_seed(Ci + Co + H)
+    x = (torch.rand(1, T, H, H, Ci, generator=g, device=dev) * 2 - 1).bfloat16()
+    dy = (torch.rand(1, T, H, H, Co, generator=g, device=dev) * 2 - 1).bfloat16()
+    w = torch.randn(Co, Ci, 3, 3, 3, generator=g, device=dev) / (27 * Ci) ** 0.5
+    wf = ops._pack_weight_now(w, Co, Ci, 27, Ci, Co, False, torch.bfloat16)
+    wb = ops._pack_weight_now(w, Co, Ci, 27, Ci, Co, True, torch.bfloat16)
+    d = ops._desc(1, [T, H, H], Ci, [T, H, H], Co, [3, 3, 3], [1, 1, 1], [1, 1, 1],
+                  ops._DT[torch.bfloat16])
+    st = ops._stream(x)
+    for name, src, wt, shp in (("vd_conv3d_fwd", x, wf, Co), ("vd_conv3d_bwd_data", dy, wb, Ci)):
+        outs = []
+        for _ in range(12):
+            o = torch.empty(1, T, H, H, shp, dtype=torch.bfloat16, device=dev)
+            if name == "vd_conv3d_fwd":
+                _lib.call(name, d, src.data_ptr(), wt.data_ptr(), None, None, None, o.data_ptr(), st)
+            else:
+                _lib.call(name, d, src.data_ptr(), wt.data_ptr(), o.data_ptr(), st)
+            outs.append(o)
+        torch.cuda.synchronize()
+        bad = [i for i, o in enumerate(outs) if not torch.equal(o, outs[0])]
+        assert not bad, (name, shape, bad)
+
+
 def _conv_vs_oracle(case, dtype):
     from vdiff import ops
     shape, Co, k, stride, pad = CASES[case]

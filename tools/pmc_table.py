@@ -1,5 +1,6 @@
 """Per-kernel mean of every PMC counter found under a rocprofv3 output tree (csv):
-  python tools/pmc_table.py gpurun_out/pmcf  -> markdown table, one row per (run dir, kernel)."""
+  python tools/pmc_table.py gpurun_out/pmcf [name substring, default attn_fwd]
+  -> markdown table, one row per (run dir, kernel)."""
 import csv
 import glob
 import os
@@ -7,6 +8,7 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1]
+flt = sys.argv[2] if len(sys.argv) > 2 else "attn_fwd"
 rows = defaultdict(lambda: defaultdict(list))
 for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     run = os.path.relpath(path, root).split(os.sep)[0]
@@ -19,7 +21,7 @@ for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recur
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
     for key, cs in per.items():
         kn = names[key]
-        if "attn_fwd" not in kn:
+        if flt not in kn:
             continue
         short = kn.split("(")[0].replace("void ", "")[:60]
         for c, v in cs.items():
