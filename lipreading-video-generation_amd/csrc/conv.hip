@@ -1505,34 +1505,60 @@ __global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
       for (int r = 0; r < 4; ++r)
         Cs[(16 * (NI * wave + i) + fq * 4 + r) * LDC + 16 * j + fr] = acc[i][j][r];
   __syncthreads();
-  const bool vec = (g.N % 8 == 0) && (g.dNs % 8 == 0);
-  for (int v = tid; v < 128 * BN / 8; v += 64 * NW) {
-    const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+  // every thread stores the same 8-channel chunk of 4 rows (256 threads, 8 chunks per row):
+  // its bias + per-(b, co) add is loaded once, and the residual rows are all requested before
+  // the first store (round 6: the per-element scalar adds and the serialised residual loads took
+  // 35 us of the 105 us of a 64->64 ResBlock conv at 16x128x128, tools/conv3_bench.py
+  // --epilogue)
+  constexpr int ITER = 128 * BN / 8 / (64 * NW);
+  const int cq = tid % (BN / 8), n = n0 + cq * 8;
+  const int lim = g.N - n < 8 ? g.N - n : 8;
+  float cadd[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cadd[e] = 0.f;
+  if (lim == 8) {
+    float tv[8];
+    if (bias) {
+      load8(bias + n, tv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cadd[e] += tv[e];
+    }
+    if (chan_add) {
+      load8(chan_add + (int64_t)b * g.N + n, tv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cadd[e] += tv[e];
+    }
+  } else {
+    for (int e = 0; e < lim; ++e)
+      cadd[e] = (bias ? bias[n + e] : 0.f) + (chan_add ? chan_add[(int64_t)b * g.N + n + e] : 0.f);
+  }
+  const bool vec = lim == 8 && (g.dNs % 8 == 0);
+  int64_t mrow[ITER];
+  float rv[ITER][8];
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int r = tid / (BN / 8) + k * (64 * NW / (BN / 8));
     const int t = t0 + r / (kHoH * kHoW), h = h0 + (r / kHoW) % kHoH, w = w0 + r % kHoW;
-    const int n = n0 + c;
-    if (t >= g.dT || h >= g.dH || n >= g.N) continue;
-    const int64_t m = (((int64_t)b * g.dT + t) * g.dH + h) * g.dW + w;
+    mrow[k] = (t < g.dT && h < g.dH && lim > 0) ? (((int64_t)b * g.dT + t) * g.dH + h) * g.dW + w
+                                                : -1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rv[k][e] = 0.f;
+    if (residual && vec && mrow[k] >= 0) load8(residual + mrow[k] * g.dNs + n, rv[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    if (mrow[k] < 0) continue;
+    const int r = tid / (BN / 8) + k * (64 * NW / (BN / 8));
     float o[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + c + e];
-    const int lim = g.N - n < 8 ? g.N - n : 8;
-    if (bias)
-      for (int e = 0; e < lim; ++e) o[e] += bias[n + e];
-    if (chan_add)
-      for (int e = 0; e < lim; ++e) o[e] += chan_add[(int64_t)b * g.N + n + e];
-    bf16_t* out = dst + m * g.dNs + n;
+    for (int e = 0; e < 8; ++e) o[e] = Cs[r * LDC + cq * 8 + e] + cadd[e] + rv[k][e];
+    bf16_t* out = dst + mrow[k] * g.dNs + n;
     if (vec) {
-      if (residual) {
-        float rv[8];
-        load8(residual + m * g.dNs + n, rv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += rv[e];
-      }
       store8(out, o);
     } else {
       for (int e = 0; e < lim; ++e) {
         float val = o[e];
-        if (residual) val += bf2f(residual[m * g.dNs + n + e]);
+        if (residual) val += bf2f(residual[mrow[k] * g.dNs + n + e]);
         out[e] = f2bf(val);
       }
     }

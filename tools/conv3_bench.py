@@ -38,6 +38,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--T", type=int, default=16)
+    ap.add_argument("--cold", action="store_true",
+                    help="flush L2 / Infinity Cache (a 1 GiB fill) before every timed launch and "
+                         "time launches one by one (the in-model state: inputs not re-read)")
+    ap.add_argument("--epilogue", action="store_true",
+                    help="forward with bias + per-(b, co) add + residual, as a ResBlock conv")
     a = ap.parse_args()
     modes = [int(m) for m in a.modes.split(",")]
     lib = _lib.lib()
@@ -49,6 +54,7 @@ def main():
     dirs = ["fwd", "bwd"] if a.dir == "both" else [a.dir]
     tot = {(d, m): 0.0 for d in dirs for m in modes}
     dt = ops._DT[torch.bfloat16]
+    flush = torch.empty(1 << 28, dtype=torch.float32, device="cuda") if a.cold else None
     for Ci, Co, H, per in shapes:
         g = torch.Generator(device="cuda").manual_seed(Ci * 7 + Co + H)
         x = (torch.rand(1, T, H, H, Ci, generator=g, device="cuda") * 2 - 1).bfloat16()
@@ -61,9 +67,14 @@ def main():
         y = torch.empty(1, T, H, H, Co, dtype=torch.bfloat16, device="cuda")
         dx = torch.empty(1, T, H, H, Ci, dtype=torch.bfloat16, device="cuda")
         flop = 2.0 * T * H * H * Co * 27 * Ci
+        bias = torch.randn(Co, generator=g, device="cuda") if a.epilogue else None
+        ca = torch.randn(1, Co, generator=g, device="cuda") if a.epilogue else None
+        res = torch.randn(1, T, H, H, Co, generator=g, device="cuda").bfloat16() if a.epilogue \
+            else None
+        ptr = lambda t: None if t is None else t.data_ptr()
         runs = {
-            "fwd": lambda: _lib.call("vd_conv3d_fwd", d, x.data_ptr(), wf.data_ptr(), None, None,
-                                     None, y.data_ptr(), st),
+            "fwd": lambda: _lib.call("vd_conv3d_fwd", d, x.data_ptr(), wf.data_ptr(), ptr(bias),
+                                     ptr(ca), ptr(res), y.data_ptr(), st),
             "bwd": lambda: _lib.call("vd_conv3d_bwd_data", d, dy.data_ptr(), wb.data_ptr(),
                                      dx.data_ptr(), st)}
         outs = {"fwd": y, "bwd": dx}
@@ -77,6 +88,18 @@ def main():
                     torch.cuda.synchronize()
                     if r == 0:
                         ref[m] = outs[dname].float().clone()
+                    if a.cold:
+                        ts = []
+                        for _ in range(a.reps):
+                            flush.fill_(1.0)
+                            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                            ev[0].record()
+                            runs[dname]()
+                            ev[1].record()
+                            torch.cuda.synchronize()
+                            ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
+                        times[m].append(statistics.median(ts))
+                        continue
                     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                     ev[0].record()
                     for _ in range(a.reps):
