@@ -769,9 +769,15 @@ def main():
                                 "warmup_steps": args.warmup, "timed_steps": args.steps,
                                 "note": "not the reference's hyperparameter when lr != 1e-2: "
                                         "train.py:102 trains at 1e-2, where this model's loss "
-                                        "spikes and it collapses to outputting 0 (as at 1e-3); "
-                                        "1e-4 is the rate at which it learns, and the kernels "
-                                        "run 4 % slower on its operands (DESIGN section 5)"}
+                                        "spikes and it collapses to outputting 0 (as at 1e-3) "
+                                        "-- product-only evidence: the oracle cannot run the "
+                                        "config-2 model for hundreds of steps on the host; at "
+                                        "1e-4 it learns over ~300 steps (profiles/"
+                                        "r05_train_curve.txt), but this short timed window "
+                                        "stays on the ~1.0 loss plateau; the kernels run ~4 % "
+                                        "slower on its operands than at 1e-3 (DESIGN section 5); "
+                                        "five bf16 steps at 1e-4 are pinned to the reference "
+                                        "(tests/test_gpu_modules.py)"}
         log(f"train: {ms:.1f} ms/step, {result['value']:.3f} frames/s, loss {float(loss):.4f}, "
             f"model {result['model_tflops_per_gpu']} TFLOP/s/GPU (3x fwd)")
         for r in rows:

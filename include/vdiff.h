@@ -317,6 +317,12 @@ int vd_attention_set_config(int cfg);
  * counterpart: the reference materialises T x T scores (unet.py:361-365 per regrouped
  * sequence). */
 int vd_attention_short_path(const vd_attn_desc* d);
+/* The backward's decision on the real buffers: 1 when vd_attention_bwd will run the fused short
+ * kernel for these pointers (every buffer 16-B aligned), 0 when it takes the flash dQ + dK/dV
+ * kernels, which need the workspace of vd_attention_bwd_workspace_size. */
+int vd_attention_bwd_short_path(const vd_attn_desc* d, const void* q, const void* k,
+                                const void* v, const void* o, const void* dout, const void* dq,
+                                const void* dk, const void* dv);
 int vd_attention_set_short(int on);
 /* dout uses the o_* strides; dq/dk/dv use the q/k/v strides (so they can be
  * written straight into a d(qkv) buffer) and are OVERWRITTEN. */

@@ -2753,6 +2753,22 @@ int vd_attention_short_path(const vd_attn_desc* d) {
   return g_short.load() && vd::short_attn_ok(d, kAligned, kAligned, kAligned, kAligned) ? 1 : 0;
 }
 
+// the backward's own decision on the real buffers (advisor r05: a descriptor-only check could
+// pick the short kernel for misaligned buffers, which then refused the call)
+static bool short_bwd_ok(const vd_attn_desc* d, const void* q, const void* k, const void* v,
+                         const void* o, const void* dout, const void* dq, const void* dk,
+                         const void* dv) {
+  if (!g_short.load() || !d || check_attn(d) || !vd::short_attn_ok(d, q, k, v, o)) return false;
+  return ((reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
+           reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) % 16) == 0;
+}
+
+int vd_attention_bwd_short_path(const vd_attn_desc* d, const void* q, const void* k,
+                                const void* v, const void* o, const void* dout, const void* dq,
+                                const void* dk, const void* dv) {
+  return short_bwd_ok(d, q, k, v, o, dout, dq, dk, dv) ? 1 : 0;
+}
+
 int vd_attention_set_short(int on) { return g_short.exchange(on ? 1 : 0); }
 
 int vd_attention_fwd(const vd_attn_desc* d, const void* q, const void* k, const void* v, void* o,
@@ -2800,7 +2816,7 @@ int vd_attention_bwd_dkdv(const vd_attn_desc* d, const void* q, const void* k, c
 int vd_attention_bwd(const vd_attn_desc* d, const void* q, const void* k, const void* v,
                      const void* o, const void* dout, const float* lse, void* dq, void* dk,
                      void* dv, void* workspace, void* stream) {
-  if (g_short.load() && d && !check_attn(d) && vd::short_attn_ok(d, q, k, v, o)) {
+  if (short_bwd_ok(d, q, k, v, o, dout, dq, dk, dv)) {
     VD_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv, "null tensor");
     return vd::short_attn_bwd(d, q, k, v, o, dout, lse, dq, dk, dv, VD_STREAM(stream));
   }

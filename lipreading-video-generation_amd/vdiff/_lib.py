@@ -110,6 +110,7 @@ _SIGS = {
                               _vp]),
     "vd_gelu_tanh": (_i, [_vp, _vp, _i64, _i, _vp]),
     "vd_attention_short_path": (_i, [C.POINTER(AttnDesc)]),
+    "vd_attention_bwd_short_path": (_i, [C.POINTER(AttnDesc)] + [C.c_void_p] * 8),
     "vd_attention_set_short": (_i, [_i]),
     "vd_mse_loss_workspace_size": (_sz, [_i64]),
     "vd_mse_loss": (_i, [_vp, _vp, _i64, _i, _vp, _vp, _sz, _vp]),

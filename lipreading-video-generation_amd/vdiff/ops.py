@@ -269,7 +269,10 @@ def silu(x):
 class MSELossFn(torch.autograd.Function):
     """mean((pred - target)^2) (train.py:103, 130: nn.MSELoss()(noise_pred, noise)) on
     vd_mse_loss: a fixed-order two-launch reduction, so the loss has the same bits eager and
-    replayed from a HIP graph; the gradient is vd_mse_loss_bwd."""
+    replayed from a HIP graph; the gradient is vd_mse_loss_bwd.  The
+    denoiser's output reaches it as the reference's fp32 standard-layout tensor
+    (UNetModel.forward ends in .type(x.dtype).contiguous(): 3 channels, 0.8 M elements at
+    config 2, a few microseconds), so the .to / .contiguous below are no-ops there."""
 
     @staticmethod
     def forward(ctx, pred, target):
@@ -931,9 +934,12 @@ class AttentionFn(torch.autograd.Function):
         for (d, qo, ko, vo, oo), lse in zip(launches, lses):
             st = _stream(qkv)
             ev = _timer.begin() if _timer is not None and _timer.attention else None
-            if _lib.lib().vd_attention_short_path(d):
+            ptrs = (base + qo * es, base + ko * es, base + vo * es, obase + oo * es,
+                    dobase + oo * es, dbase + qo * es, dbase + ko * es, dbase + vo * es)
+            if _lib.lib().vd_attention_bwd_short_path(d, *ptrs):
                 # short sequences (temporal mode, <= 32 tokens): ONE fused dQ / dK / dV
-                # launch, no workspace (attn_short.hip)
+                # launch, no workspace (attn_short.hip); decided on these very buffers, so it
+                # agrees with vd_attention_bwd (advisor r05)
                 _lib.call("vd_attention_bwd", d, base + qo * es, base + ko * es, base + vo * es,
                           obase + oo * es, dobase + oo * es, _p(lse), dbase + qo * es,
                           dbase + ko * es, dbase + vo * es, None, st)

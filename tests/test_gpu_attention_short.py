@@ -116,3 +116,44 @@ def test_short_path_predicate():
                         (16, _lib.VD_F32, 0)):
         (d, *_), = ops._attn_desc(1, T * 8, 64, 1, 64, "temporal", (T, 8, 1), dt, True)
         assert lib.vd_attention_short_path(d) == want, (T, dt)
+
+
+def test_backward_with_misaligned_gradient_falls_back_to_flash():
+    """Advisor r05: the backward decides on the real buffers.  With aligned q / k / v / o (the
+    forward on the short kernel) but a dout that is not 16-B aligned, vd_attention_bwd_short_path
+    says 0 and vd_attention_bwd runs the flash dQ + dK/dV kernels with a workspace, giving the
+    gradients of the aligned call (which takes the fused short kernel) within bf16 rounding."""
+    from vdiff import _lib, ops
+    lib = _lib.lib()
+    B, C, T, HW = 1, 64, 16, 24
+    N = T * HW
+    (d, qo, ko, vo, oo), = ops._attn_desc(B, N, C, 1, C, "temporal", (T, HW, 1), _lib.VD_BF16,
+                                          True)
+    g = torch.Generator(device=dev).manual_seed(3)
+    qkv = (torch.randn(B, N, 3 * C, generator=g, device=dev)).bfloat16()
+    out = torch.empty(B, N, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(d.nseq * d.seq_len, dtype=torch.float32, device=dev)
+    es = 2
+    base = qkv.data_ptr()
+    st = ops._stream(qkv)
+    _lib.call("vd_attention_fwd_ws", d, base + qo * es, base + ko * es, base + vo * es,
+              out.data_ptr(), lse.data_ptr(), None, 0, st)
+    dsrc = torch.randn(B * N * C, generator=g, device=dev).bfloat16()
+    dout_buf = torch.zeros(B * N * C + 8, dtype=torch.bfloat16, device=dev)
+    grads = {}
+    for name, off in (("aligned", 0), ("misaligned", 1)):
+        dout = dout_buf[off:off + B * N * C]
+        dout.copy_(dsrc)
+        dq = torch.zeros(B, N, 3 * C, dtype=torch.bfloat16, device=dev)
+        ptrs = (base + qo * es, base + ko * es, base + vo * es, out.data_ptr(), dout.data_ptr(),
+                dq.data_ptr() + qo * es, dq.data_ptr() + ko * es, dq.data_ptr() + vo * es)
+        short = lib.vd_attention_bwd_short_path(d, *ptrs)
+        assert short == (1 if off == 0 else 0), (name, short)
+        ws = torch.empty(max(1, lib.vd_attention_bwd_workspace_size(d)), dtype=torch.uint8,
+                         device=dev)
+        _lib.call("vd_attention_bwd", d, ptrs[0], ptrs[1], ptrs[2], ptrs[3], ptrs[4],
+                  lse.data_ptr(), ptrs[5], ptrs[6], ptrs[7], ws.data_ptr(), st)
+        grads[name] = dq.float()
+    torch.cuda.synchronize()
+    assert grads["aligned"].abs().max() > 0
+    assert rel_l2(grads["misaligned"], grads["aligned"]) < 2e-2
