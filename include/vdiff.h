@@ -234,6 +234,10 @@ int vd_conv3d_bwd_weight_det(const vd_conv_desc* d, const void* x, const void* d
  * channels or N <= 64).  Results are identical up to fp32 summation order.
  * Process-wide; returns the previous mode, or -2 for an invalid one.  Initial value from env
  * VDIFF_CONV_HALO.  No reference counterpart: an A/B and test hook. */
+/* Which kernel computes the kw-strip (3x3x3 / 3x3 stride-1 bf16) weight gradients: 1 (default)
+ * the round-6 kernel with the ring stages unrolled, 0 the round-5 kernel; same tiles and
+ * summation order (bit-identical results).  Returns the previous mode (A/B, tests). */
+int vd_conv_set_wgrad(int mode);
 int vd_conv_set_halo(int mode);
 
 /* ---- Conv glue ---------------------------------------------------------

@@ -1087,6 +1087,266 @@ __global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
   }
 }
 
+// ---- round 6: the kw-strip weight gradient with its step loop unrolled by the ring depth.
+// wgrad_dma_kernel spent ~150 VALU and ~60 SALU instructions per 24-MFMA step (SQ_INSTS_VALU
+// 7380 per wave, 64->64 at 16x128x128): every transposed fragment read recomputed its
+// swizzled address from the runtime ring stage, and the X strip's source pixels were found by
+// divergent wrap loops.  Here the ring stage is a compile-time constant (the loop body is
+// unrolled NST times), so every ds_read_b64_tr_b16 is a precomputed per-lane base plus an
+// immediate, and an X piece's source pixel is the step's first pixel plus a per-lane constant
+// (same-size stride-1 conv: pixel = m + (kt - pt) H W + (kh - ph) W + row * wc + j - pw) with a
+// branch-free bounds test.  Same tiles, DMA pieces and summation order as wgrad_dma_kernel.
+// KIND 0: kw strip, a step is R = 64 / Wo whole image rows; 1: kw strip, a step is one 64-pixel
+// row segment (W % 64 == 0); 2: 1x1 stride-1 unpadded conv (X rows = dY rows, one tap).
+template <int RW, int COT, int NST, int KIND>
+__global__ __launch_bounds__(kThreads, 2) void wgrad_strip_kernel(WgtGeom g, int wc,
+                                                                  const bf16_t* __restrict__ x,
+                                                                  const bf16_t* __restrict__ dy,
+                                                                  float* __restrict__ dw) {
+  constexpr int PY = COT / 32, PX = RW / 32;  // pieces per wave per step
+  constexpr int PIECES = PY + PX;
+  constexpr int Y_BYTES = COT * 128, STAGE = (COT + RW) * 128;
+  constexpr bool ROW1 = KIND == 1, ONE = KIND == 2;
+  constexpr int WTM = COT / 2, NI = WTM / 16, NT = ONE ? 1 : 3;
+  static_assert(!ONE || RW == 64, "1x1: the X tile is the step's 64 pixels");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int co_tiles = (g.Co + COT - 1) / COT, ci_tiles = (g.Ci + 63) / 64;
+  int bid, wsplit;
+  if (!wg_tile(g, &bid, &wsplit)) return;  // padding of the XCD-aware grid
+  const int cot = bid % co_tiles; bid /= co_tiles;
+  const int cit = bid % ci_tiles; bid /= ci_tiles;
+  const int tab = bid;  // (kt, kh) index
+  const int ta = tab / g.kh, tb = tab % g.kh;
+  const int co0 = cot * COT, ci0 = cit * 64;
+  const int64_t mbeg = (int64_t)wsplit * g.m_per_split;
+  int64_t mend = mbeg + g.m_per_split;
+  if (mend > g.M) mend = g.M;
+  if (mbeg >= mend) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane >> 3, pc = lane & 7;
+  const int R = 64 / wc, SW = wc + 2;
+  const int HWi = g.Hi * g.Wi;
+  const int delta = (ta - g.pt) * HWi + (tb - g.ph) * g.Wi;  // source pixel of output pixel 0
+  int y_off[PY];
+  bool y_ok[PY];
+#pragma unroll
+  for (int i = 0; i < PY; ++i) {
+    const int pi = wave * PY + i;
+    const int p = (pi & 7) * 8 + lr;
+    const int c = pc ^ wg_swz(p);
+    const int col = co0 + (pi >> 3) * 64 + c * 8;
+    y_ok[i] = col < g.Co;
+    y_off[i] = (p * g.yCs + col) * 2;  // + step pixel * yCs * 2
+  }
+  // X pieces: strip row sr -> step row rr and strip column j (pixel w0 + j - pw)
+  int x_rr[PX], x_j[PX], x_off[PX];
+  bool x_ok[PX];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    const int sr = (wave * PX + i) * 8 + lr;
+    const int col = ci0 + (pc ^ wg_swz(sr)) * 8;
+    if constexpr (ONE) {  // X row sr = the step's pixel sr
+      x_rr[i] = 0;
+      x_j[i] = sr;
+      x_ok[i] = col < g.Ci;
+      x_off[i] = (sr * g.xCs + col) * 2;
+      continue;
+    }
+    const int rr = sr / SW, j = sr - rr * SW;
+    x_rr[i] = rr;
+    x_j[i] = j - g.pw;
+    x_ok[i] = rr < R && col < g.Ci;
+    x_off[i] = ((delta + rr * wc + j - g.pw) * g.xCs + col) * 2;  // + step pixel * xCs * 2
+  }
+  const rsrc_t rs_y = make_rsrc(dy, (uint32_t)(g.M * g.yCs * 2));
+  const rsrc_t rs_x = make_rsrc(x, (uint32_t)((int64_t)g.B * g.Ti * g.Hi * g.Wi * g.xCs * 2));
+
+  // first pixel of the step being issued (incremental): w, h, t of its first row
+  int cw, chh, ct;
+  {
+    int64_t m = mbeg;
+    cw = (int)(m % g.Wo); m /= g.Wo;
+    chh = (int)(m % g.Ho); m /= g.Ho;
+    ct = (int)(m % g.To);
+  }
+  const int nsteps = (int)((mend - mbeg + 63) / 64);
+  const int ms0 = (int)mbeg, me = (int)mend;
+  auto issue = [&](int s, int stage) {
+    char* st = smem + stage * STAGE;
+    const bool live = s < nsteps;
+    const int ms = ms0 + s * 64;
+#pragma unroll
+    for (int i = 0; i < PY; ++i) {
+      const bool ok = live & y_ok[i] & (ms + ((wave * PY + i) & 7) * 8 + lr < me);
+      dma_lds<16>(rs_y, lds_addr(st + (wave * PY + i) * 1024),
+                  ok ? (uint32_t)(y_off[i] + ms * g.yCs * 2) : 0x80000000u);
+    }
+    if constexpr (ONE) {
+#pragma unroll
+      for (int i = 0; i < PX; ++i) {
+        const bool ok = live & x_ok[i] & (ms + x_j[i] < me);
+        dma_lds<16>(rs_x, lds_addr(st + Y_BYTES + (wave * PX + i) * 1024),
+                    ok ? (uint32_t)(x_off[i] + ms * g.xCs * 2) : 0x80000000u);
+      }
+      return;
+    } else if constexpr (ROW1) {  // every strip row is the step's own output row: (ct, chh) uniform
+      const int ti = ct + ta - g.pt, hi = chh + tb - g.ph;
+      const bool row_ok = live & (ms < me) & ((unsigned)ti < (unsigned)g.Ti) &
+                          ((unsigned)hi < (unsigned)g.Hi);
+#pragma unroll
+      for (int i = 0; i < PX; ++i) {
+        const int wi = cw + x_j[i];
+        const bool ok = row_ok & x_ok[i] & ((unsigned)wi < (unsigned)g.Wi);
+        dma_lds<16>(rs_x, lds_addr(st + Y_BYTES + (wave * PX + i) * 1024),
+                    ok ? (uint32_t)(x_off[i] + ms * g.xCs * 2) : 0x80000000u);
+      }
+    } else {
+      // R = 64 / Wo whole rows per step (cw = 0): each row's validity is uniform (scalar);
+      // a lane picks its strip row's (R <= 4: the launcher takes only 64 / Wo <= Ho)
+      bool rok[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int h = chh + r, t = ct;
+        const bool wrap = h >= g.Ho;
+        h -= wrap ? g.Ho : 0;
+        t += wrap ? 1 : 0;
+        t -= t == g.To ? g.To : 0;  // next clip of the batch: its frame 0
+        const int ti = t + ta - g.pt, hi = h + tb - g.ph;
+        rok[r] = (r < R) & live & (ms + r * wc < me) & ((unsigned)ti < (unsigned)g.Ti) &
+                 ((unsigned)hi < (unsigned)g.Hi);
+      }
+#pragma unroll
+      for (int i = 0; i < PX; ++i) {
+        const int rr = x_rr[i];
+        const bool row = rr == 0 ? rok[0] : rr == 1 ? rok[1] : rr == 2 ? rok[2] : rok[3];
+        const bool ok = row & x_ok[i] & ((unsigned)x_j[i] < (unsigned)g.Wi);
+        dma_lds<16>(rs_x, lds_addr(st + Y_BYTES + (wave * PX + i) * 1024),
+                    ok ? (uint32_t)(x_off[i] + ms * g.xCs * 2) : 0x80000000u);
+      }
+    }
+    if (live) {  // advance by 64 pixels (scalar)
+      cw += 64;
+      while (cw >= g.Wo) {
+        cw -= g.Wo;
+        if (++chh == g.Ho) {
+          chh = 0;
+          if (++ct == g.To) ct = 0;
+        }
+      }
+    }
+  };
+
+  // wave tile: co [WTM wm, +WTM) x ci [32 wn, +32) x 3 taps
+  const int wm = wave & 1, wn = wave >> 1;
+  f32x4 acc[NT][NI][2];
+#pragma unroll
+  for (int tc = 0; tc < NT; ++tc)
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[tc][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4, q4 = fr >> 2, p4 = fr & 3;
+  // LDS byte addresses (stage 0) of every transposed fragment read (loop-invariant); a read of
+  // stage u adds u * STAGE as the instruction's immediate offset
+  const uint32_t lb = lds_addr(smem);
+  uint32_t abase[2][2][NI], xbase[2][2][NT][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      const int p = 32 * ks + 8 * fq + q4 + 4 * hl;
+      const int sp = ONE ? p : (p / wc) * SW + p % wc;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int c = wm * WTM + 16 * i + 4 * p4;
+        abase[ks][hl][i] = lb + ((c >> 6) * 4096 + wg_off(p, c & 63)) * 2;
+      }
+#pragma unroll
+      for (int tc = 0; tc < NT; ++tc)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          xbase[ks][hl][tc][j] = lb + Y_BYTES + wg_off(sp + tc, wn * 32 + 16 * j + 4 * p4) * 2;
+    }
+
+  vm_drain();
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s, s);
+  for (int s0 = 0; s0 < nsteps; s0 += NST) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) asm volatile("" : "+v"(abase[ks][hl][i]));
+#pragma unroll
+        for (int tc = 0; tc < NT; ++tc)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(xbase[ks][hl][tc][j]));
+      }
+#pragma unroll
+    for (int u = 0; u < NST; ++u) {
+      const int s = s0 + u;
+      if (s >= nsteps) break;
+      vm_lgk_wait_barrier<(NST - 2) * PIECES>();
+      issue(s + NST - 1, (u + NST - 1) % NST);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(uintptr_t)(abase[ks][0][i] + u * STAGE));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(uintptr_t)(abase[ks][1][i] + u * STAGE));
+          af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int tc = 0; tc < NT; ++tc) {
+          bf16x8 bfr[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_bf16x4*)(uintptr_t)(xbase[ks][0][tc][j] + u * STAGE));
+            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_bf16x4*)(uintptr_t)(xbase[ks][1][tc][j] + u * STAGE));
+            bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[tc][i][j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[tc][i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  vm_drain();
+  const int taps = g.kt * g.kh * g.kw;
+  const int64_t krow = (int64_t)taps * g.Ci;
+#pragma unroll
+  for (int tc = 0; tc < NT; ++tc) {
+    const int tap = ONE ? 0 : tab * g.kw + tc;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = ci0 + wn * 32 + 16 * j + fr;
+        if (ci >= g.Ci) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wm * WTM + 16 * i + fq * 4 + r;
+          if (co < g.Co)
+            wg_out(g, dw, wsplit, (int64_t)co * krow + (int64_t)tap * g.Ci + ci,
+                   acc[tc][i][j][r]);
+        }
+      }
+  }
+}
+
 // ----------------------------------------------------------------- bf16 implicit GEMM, LDS-DMA ring
 // Same GEMM and tap-major K walk as igemm_bf16_kernel, but the A rows (gathered pixels) and
 // B rows (packed weights) go global -> LDS by buffer_load ... lds, in 1-KiB pieces of 8
@@ -1581,6 +1841,13 @@ std::atomic<int> g_halo_mode{[] {
   return e ? atoi(e) : 2;
 }()};
 int conv_halo_mode() { return g_halo_mode.load(std::memory_order_relaxed); }
+// kw-strip weight-gradient kernel: 1 (default) wgrad_strip_kernel, 0 the round-5
+// wgrad_dma_kernel (A/B; vd_conv_set_wgrad, VDIFF_WGRAD_STRIP)
+std::atomic<int> g_wgrad_mode{[] {
+  const char* e = getenv("VDIFF_WGRAD_STRIP");
+  return e ? atoi(e) : 1;
+}()};
+
 // Channels per halo step for this conv, 0 = the gathered-tile kernel: 64-channel steps (80 KiB,
 // two workgroups per CU) at the 32x32 level and from 128 reduction channels on, 32-channel
 // steps (40 KiB, four per CU) otherwise; VDIFF_CONV_HALO_KS forces one (A/B).  sC = the GEMM's
@@ -1930,6 +2197,14 @@ int vd_conv3d_fwd(const vd_conv_desc* d, const void* x, const void* w_fwd, const
   });
 }
 
+int vd_conv_set_wgrad(int mode) {
+  if (mode < 0 || mode > 1) {
+    (void)vd::fail(VD_EINVAL, "conv wgrad mode %d (0, 1)", mode);
+    return -2;
+  }
+  return g_wgrad_mode.exchange(mode);
+}
+
 int vd_conv_set_halo(int mode) {
   if (mode < 0 || mode > 2) {
     (void)vd::fail(VD_EINVAL, "conv halo mode %d (0, 1, 2)", mode);
@@ -2118,7 +2393,26 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
   } while (0)
     // 64 x 64 tiles, double-buffered (40 KiB at RW = 96: three workgroups per CU).
     // Measured against COT = 128 and a three-stage ring: both slower (tools/conv_ab.sh).
-    if (one && cot == 192 && w1_nst >= 4) VD_WGD(64, 192, 4, true);
+#define VD_WG1(COT, NST)                                                                   \
+  do {                                                                                     \
+    auto kern = wgrad_strip_kernel<64, COT, NST, 2>;                                       \
+    const int lds = NST * (COT + 64) * 128;                                                \
+    (void)hipFuncSetAttribute((const void*)kern,                                           \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
+    kern<<<grid, kThreads, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);     \
+  } while (0)
+    const bool v2 = g_wgrad_mode.load(std::memory_order_relaxed) == 1;
+    if (one && v2) {  // round 6: unrolled stages (the 1x1 form of wgrad_strip_kernel)
+      if (cot == 192 && w1_nst >= 4) VD_WG1(192, 4);
+      else if (cot == 192) VD_WG1(192, 2);
+      else if (cot == 128 && w1_nst >= 4) VD_WG1(128, 4);
+      else if (cot == 128) VD_WG1(128, 2);
+      else if (w1_nst >= 6) VD_WG1(64, 6);
+      else if (w1_nst >= 4) VD_WG1(64, 4);
+      else VD_WG1(64, 2);
+    }
+#undef VD_WG1
+    else if (one && cot == 192 && w1_nst >= 4) VD_WGD(64, 192, 4, true);
     else if (one && cot == 192) VD_WGD(64, 192, 2, true);
     else if (one && cot == 128 && w1_nst >= 4) VD_WGD(64, 128, 4, true);
     else if (one && cot == 128) VD_WGD(64, 128, 2, true);
@@ -2126,6 +2420,30 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     else if (one && w1_nst >= 4) VD_WGD(64, 64, 4, true);
     else if (one) VD_WGD(64, 64, 2, true);
     else if (plane) VD_WGD(224, 64, 2, false, true);
+    else if (v2) {  // round 6: unrolled stages
+#define VD_WGS(RW, COT, NST)                                                               \
+  do {                                                                                     \
+    auto kern = wc == 64 ? wgrad_strip_kernel<RW, COT, NST, 1>                             \
+                         : wgrad_strip_kernel<RW, COT, NST, 0>;                            \
+    const int lds = NST * (COT + RW) * 128;                                                \
+    (void)hipFuncSetAttribute((const void*)kern,                                           \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
+    kern<<<grid, kThreads, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);     \
+  } while (0)
+      if (cot == 128 && w3_nst >= 3 && rows <= 96) VD_WGS(96, 128, 3);
+      else if (cot == 128 && w3_nst >= 3 && rows <= 128) VD_WGS(128, 128, 3);
+      else if (cot == 128 && w3_nst >= 3) VD_WGS(192, 128, 3);
+      else if (cot == 128 && rows <= 96) VD_WGS(96, 128, 2);
+      else if (cot == 128 && rows <= 128) VD_WGS(128, 128, 2);
+      else if (cot == 128) VD_WGS(192, 128, 2);
+      else if (w3_nst >= 3 && rows <= 96) VD_WGS(96, 64, 3);
+      else if (w3_nst >= 3 && rows <= 128) VD_WGS(128, 64, 3);
+      else if (w3_nst >= 3) VD_WGS(192, 64, 3);
+      else if (rows <= 96) VD_WGS(96, 64, 2);
+      else if (rows <= 128) VD_WGS(128, 64, 2);
+      else VD_WGS(192, 64, 2);
+#undef VD_WGS
+    }
     else if (cot == 128 && w3_nst >= 3 && rows <= 96) VD_WGD(96, 128, 3, false);
     else if (cot == 128 && w3_nst >= 3 && rows <= 128) VD_WGD(128, 128, 3, false);
     else if (cot == 128 && w3_nst >= 3) VD_WGD(192, 128, 3, false);

@@ -75,6 +75,7 @@ _SIGS = {
     "vd_channel_sums": (_i, [_vp, _i, _i64, _i, _i, _i, _vp, _vp, _vp]),
     "vd_conv_pack_weight": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "vd_conv_pack_weights": (_i, [_vp, _i, _i64, _i, _vp]),
+    "vd_conv_set_wgrad": (_i, [C.c_int]),
     "vd_conv_set_halo": (_i, [_i]),
     "vd_conv3d_fwd": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "vd_conv3d_bwd_data": (_i, [C.POINTER(ConvDesc), _vp, _vp, _vp, _vp]),

@@ -21,7 +21,7 @@ ENV = ("VDIFF_WGRAD1", "VDIFF_WGRAD3", "VDIFF_WGRAD_QRULE", "VDIFF_WGRAD_SPLITS"
 pytestmark = pytest.mark.skipif(any(os.environ.get(e) for e in ENV),
                                 reason="non-default kernel-selection environment")
 
-# (Ci, Co, k, H = W, T) of the config-2 step (tools/wgrad_ab.py SHAPES)
+# (Ci, Co, k, H = W, T) of the config-2 step (tools/wgrad3_bench.py SHAPES)
 SHAPES = ((256, 256, 3, 32, 16), (64, 64, 3, 128, 16), (128, 128, 3, 64, 16),
           (128, 64, 3, 128, 16), (200, 64, 3, 128, 16), (512, 256, 3, 32, 16),
           (128, 128, 3, 128, 16), (256, 256, 3, 64, 16), (384, 128, 3, 64, 16),

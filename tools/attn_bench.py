@@ -82,7 +82,7 @@ if __name__ == "__main__":
         i = sys.argv.index("--only")
         only = int(sys.argv[i + 1])
         del sys.argv[i:i + 2]
-    if "--nocheck" in sys.argv:  # ablation builds (tools/exp2.sh) are wrong by design
+    if "--nocheck" in sys.argv:  # ablation builds are wrong by design
         sys.argv.remove("--nocheck")
     else:
         check()

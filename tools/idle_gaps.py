@@ -2,7 +2,7 @@
 intervals against the span from the first to the last kernel, the idle gaps between
 consecutive kernels binned by length, and the largest gaps with the kernels either side.
 This is the time a HIP-graph replay of the same work could recover at most.
-    rocprofv3 --kernel-trace --output-format csv -d gpurun_out/gap -- python3 tools/step_gap.py ...
+    rocprofv3 --kernel-trace --output-format csv -d gpurun_out/gap -- python3 bench.py --only train ...
     python tools/idle_gaps.py gpurun_out/gap/**/*kernel_trace.csv [--skip-ms 0]
 """
 import argparse
