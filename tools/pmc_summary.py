@@ -20,7 +20,7 @@ for p in glob.glob(f"{root}/p*/pmc_counter_collection.csv"):
         if flt not in names[k]:
             continue
         for c, v in cs.items():
-            rows[names[k].split("(")[0].replace("void ", "")[:70]][c].append(v)
+            rows[names[k].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:70]][c].append(v)
 for k, cs in rows.items():
     m = {c: sum(v) / len(v) for c, v in cs.items()}
     w = m.get("SQ_WAVES", 1)
