@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_strip_kernel(WgtGeom g, int
     const int rr = sr / SW, j = sr - rr * SW;
     x_rr[i] = rr;
     x_j[i] = j - g.pw;
-    x_ok[i] = rr < R && col < g.Ci;
+    x_ok[i] = rr < R && col < g.Ci && (ROW1 || (unsigned)(j - g.pw) < (unsigned)g.Wi);
     x_off[i] = ((delta + rr * wc + j - g.pw) * g.xCs + col) * 2;  // + step pixel * xCs * 2
   }
   const rsrc_t rs_y = make_rsrc(dy, (uint32_t)(g.M * g.yCs * 2));
@@ -1180,7 +1180,8 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_strip_kernel(WgtGeom g, int
     const int ms = ms0 + s * 64;
 #pragma unroll
     for (int i = 0; i < PY; ++i) {
-      const bool ok = live & y_ok[i] & (ms + ((wave * PY + i) & 7) * 8 + lr < me);
+      // (kw strips: M and every split bound are multiples of 64, so only 1x1 steps run short)
+      const bool ok = live & y_ok[i] & (!ONE || ms + ((wave * PY + i) & 7) * 8 + lr < me);
       dma_lds<16>(rs_y, lds_addr(st + (wave * PY + i) * 1024),
                   ok ? (uint32_t)(y_off[i] + ms * g.yCs * 2) : 0x80000000u);
     }
@@ -1204,32 +1205,30 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_strip_kernel(WgtGeom g, int
                     ok ? (uint32_t)(x_off[i] + ms * g.xCs * 2) : 0x80000000u);
       }
     } else {
-      // R = 64 / Wo whole rows per step (cw = 0): each row's validity is uniform (scalar);
-      // a lane picks its strip row's (R <= 4: the launcher takes only 64 / Wo <= Ho)
-      bool rok[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int h = chh + r, t = ct;
-        const bool wrap = h >= g.Ho;
-        h -= wrap ? g.Ho : 0;
-        t += wrap ? 1 : 0;
-        t -= t == g.To ? g.To : 0;  // next clip of the batch: its frame 0
-        const int ti = t + ta - g.pt, hi = h + tb - g.ph;
-        rok[r] = (r < R) & live & (ms + r * wc < me) & ((unsigned)ti < (unsigned)g.Ti) &
-                 ((unsigned)hi < (unsigned)g.Hi);
-      }
+      // R = 64 / Wo whole rows per step, all of one frame (the launcher takes this kind only
+      // when Ho % R == 0, so a 64-aligned step never crosses a frame): (ct, chh) is the step's
+      // first row, and a lane's strip row rr reads input row chh + rr + kh - ph of frame
+      // ct + kt - pt (its column range test is loop-invariant, in x_ok)
+      const int ti = ct + ta - g.pt, h0 = chh + tb - g.ph;
+      const bool t_ok = live & ((unsigned)ti < (unsigned)g.Ti);
 #pragma unroll
       for (int i = 0; i < PX; ++i) {
-        const int rr = x_rr[i];
-        const bool row = rr == 0 ? rok[0] : rr == 1 ? rok[1] : rr == 2 ? rok[2] : rok[3];
-        const bool ok = row & x_ok[i] & ((unsigned)x_j[i] < (unsigned)g.Wi);
+        const bool ok = t_ok & x_ok[i] & ((unsigned)(h0 + x_rr[i]) < (unsigned)g.Hi);
         dma_lds<16>(rs_x, lds_addr(st + Y_BYTES + (wave * PX + i) * 1024),
                     ok ? (uint32_t)(x_off[i] + ms * g.xCs * 2) : 0x80000000u);
       }
+      if (live) {  // advance by R rows
+        chh += R;
+        if (chh >= g.Ho) {
+          chh = 0;
+          if (++ct == g.To) ct = 0;
+        }
+      }
+      return;
     }
-    if (live) {  // advance by 64 pixels (scalar)
+    if (live) {  // advance by 64 pixels (scalar; Wo % 64 == 0: at most one row wrap)
       cw += 64;
-      while (cw >= g.Wo) {
+      if (cw >= g.Wo) {
         cw -= g.Wo;
         if (++chh == g.Ho) {
           chh = 0;
@@ -2401,7 +2400,9 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
     kern<<<grid, kThreads, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);     \
   } while (0)
-    const bool v2 = g_wgrad_mode.load(std::memory_order_relaxed) == 1;
+    // (KIND 0 needs whole-frame steps: Ho % (64 / Wo) == 0, else the round-5 kernel)
+    const bool v2 = g_wgrad_mode.load(std::memory_order_relaxed) == 1 &&
+                    (one || wc == 64 || d->Ho % (64 / wc) == 0);
     if (one && v2) {  // round 6: unrolled stages (the 1x1 form of wgrad_strip_kernel)
       if (cot == 192 && w1_nst >= 4) VD_WG1(192, 4);
       else if (cot == 192) VD_WG1(192, 2);

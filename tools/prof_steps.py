@@ -13,7 +13,7 @@ from prof_summary import short  # noqa: E402
 def cat(n):
     if n.startswith(("attn_", "vd_attn_")):
         return "attention (vdiff)"
-    if n.startswith(("wgrad_dma", "wgrad_finish", "conv_wgrad")):
+    if n.startswith(("wgrad_dma", "wgrad_strip", "wgrad_finish", "conv_wgrad")):
         return "conv weight gradient (vdiff)"
     if n.startswith("channel_sums"):
         return "conv bias / emb-add gradient (vdiff)"
