@@ -150,6 +150,15 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma,
                           float* dbeta, int B, int64_t S, int C, int G,
                           int silu, float drop_p, uint64_t seed, int dtype,
                           void* workspace, void* stream);
+/* The same with dx += dadd (dadd in x's layout and dtype, or NULL): x's gradient from its
+ * other consumer -- the residual branch of ResBlock (unet.py:268, skip_connection(x) + h) and
+ * AttentionBlock (unet.py:317, x + h) -- added in fp32 before dx is rounded, instead of the
+ * separate elementwise add autograd would run to accumulate the two gradients. */
+int vd_groupnorm_silu_bwd_add(const void* x, const void* dy, const void* dadd,
+                              const float* gamma, const float* beta, const float* mean,
+                              const float* rstd, void* dx, float* dgamma, float* dbeta,
+                              int B, int64_t S, int C, int G, int silu, float drop_p,
+                              uint64_t seed, int dtype, void* workspace, void* stream);
 
 /* ---- SiLU on flat tensors (time-embedding MLP, ResBlock.emb_layers:
  * unet.py:483-487, 211-217).  bwd: dx = dy * silu'(x). */

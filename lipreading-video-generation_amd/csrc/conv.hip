@@ -1569,14 +1569,18 @@ void launch_igd(const GemmGeom& g, const void* src, const void* wt, void* dst, c
 // 3-stage ring (one workgroup barrier per tap).  Transposed (bwd-data, stride 1): the same halo
 // with the tap offsets mirrored (source pixel = out + 1 - tap).  Needs W % 16 == 0; partial
 // t / h tiles are masked (zero halo rows, skipped stores).
-constexpr int kHoT = 2, kHoH = 4, kHoW = 16;                    // output tile
-constexpr int kHaT = kHoT + 2, kHaH = kHoH + 2, kHaW = kHoW + 2;  // input halo
-constexpr int kHaP = kHaT * kHaH * kHaW;                         // 432 pixels = 54 pieces
-// KS channels per step: 64 (128-B LDS rows, 80 KiB per workgroup, two per CU) or 32 (64-B
-// rows, 40 KiB, four per CU); weight ring stages NSTB (prefetch distance NSTB - 1).
-template <int NSTB, int KS>
-constexpr size_t halo_lds() { return (size_t)(kHaP + NSTB * 64) * 2 * KS + 1024; }  // + junk
-static_assert(kHaP % 16 == 0, "whole halo pieces");
+// Output tile 2 x NW x 16 pixels (t, h, w) for NW waves (two 16-pixel rows per wave): NW = 4
+// (the default) or 8 (round 6, A/B: one tile shared by 8 waves halves the weight-slice DMA per
+// output and the halo pixels per output drop from 3.4 to 2.8).
+constexpr int kHoT = 2, kHoW = 16;
+constexpr int kHaT = kHoT + 2, kHaW = kHoW + 2;
+template <int NW>
+constexpr int halo_px() { return kHaT * (NW + 2) * kHaW; }  // 432 (NW 4) / 720 (NW 8) pixels
+// KS channels per step: 64 (128-B LDS rows, 80 KiB per 4-wave workgroup, two per CU) or 32
+// (64-B rows, 40 KiB, four per CU); weight ring stages NSTB (prefetch distance NSTB - 1).
+template <int NSTB, int KS, int NW = 4>
+constexpr size_t halo_lds() { return (size_t)(halo_px<NW>() + NSTB * 64) * 2 * KS + 1024; }
+static_assert(halo_px<4>() % 16 == 0 && halo_px<8>() % 16 == 0, "whole halo pieces");
 // Round 6: every tap unrolled.  The rolled tap loop spent ~35 SALU and ~16 VALU instructions
 // per tap deriving (dt, dh, dw) by division, the ring stage and the fragment addresses
 // (SQ_INSTS_SALU 2011 per wave for 432 MFMAs, 64->64 at 16x128x128), all on the wave's path
@@ -1596,29 +1600,32 @@ __device__ __forceinline__ int h2_swz(int w) {
   else return (w >> 1) & 2;
 }
 
-template <bool TR, int KS>
-__global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
+template <bool TR, int KS, int NW>
+__global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
     GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
     bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
     const bf16_t* __restrict__ residual) {
-  constexpr int NW = 4, NSTB = 3, PD = NSTB - 1;
+  constexpr int NSTB = 3, PD = NSTB - 1, TH = NW, kHaH = TH + 2, kHaP = halo_px<NW>();
   constexpr int RB = 2 * KS, PPP = 1024 / RB, CPR = KS / 8;  // row bytes, rows per piece, chunks
   constexpr int HP = kHaP / PPP;                                // halo pieces
-  constexpr int BN = 64, NI = 8 / NW, NJ = 4, IB = BN / PPP / NW, TAPS = 27, NS = KS / 32;
+  constexpr int BN = 64, NI = 2, NJ = 4, TAPS = 27, NS = KS / 32;
+  constexpr int WP = BN / PPP, IB = WP >= NW ? WP / NW : 1;     // weight pieces per tap, per wave
   constexpr int HPW = (HP + NW - 1) / NW;                       // halo pieces per wave
-  static_assert(IB >= 1, "one weight piece per wave at least");
+  static_assert(WP % NW == 0 || NW % WP == 0, "weight pieces spread evenly");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem + kHaP * RB;
   char* junk = ring + NSTB * BN * RB;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tilesW = g.dW / kHoW, tilesH = (g.dH + kHoH - 1) / kHoH;
+  // waves that stream weight pieces (all but NW = 8 at 32-channel steps: waves 0-3)
+  const bool wl = WP >= NW || wave * IB < WP;
+  const int tilesW = g.dW / kHoW, tilesH = (g.dH + TH - 1) / TH;
   const int tilesT = (g.dT + kHoT - 1) / kHoT;
   int mt = blockIdx.x;
   const int w0 = (mt % tilesW) * kHoW;
   mt /= tilesW;
-  const int h0 = (mt % tilesH) * kHoH;
+  const int h0 = (mt % tilesH) * TH;
   mt /= tilesH;
   const int t0 = (mt % tilesT) * kHoT;
   const int b = mt / tilesT;
@@ -1661,6 +1668,7 @@ __global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
   auto issue_b = [&](int cs, int tap) {  // tap >= 27: zero fill into the free stage
     char* st = ring + (tap % NSTB) * (BN * RB);
     const int c0 = cs * KS;
+    if (!wl) return;
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const bool ok = (tap < TAPS) & (b_off[i] >= 0) & (c0 + b_c[i] < C);
@@ -1679,7 +1687,7 @@ __global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
   int abase[NI][3][NS];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int rb = NI * wave + i, tl = rb / kHoH, hl = rb % kHoH;
+    const int rb = NI * wave + i, tl = rb / TH, hl = rb % TH;
     const int line = tl * kHaH + hl;
 #pragma unroll
     for (int d = 0; d < 3; ++d)
@@ -1716,7 +1724,8 @@ __global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
 #pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
       // this tap's weights (and at tap 0 the halo) landed everywhere; stage tap-1 is free
-      vm_lgk_wait_barrier<(PD - 1) * IB>();
+      if (wl) vm_lgk_wait_barrier<(PD - 1) * IB>();
+      else vm_lgk_wait_barrier<0>();
       issue_b(cs, tap + PD);
 #pragma unroll
       for (int u = (tap == 0 ? 0 : 1); u < 2; ++u) {  // tap 0: its own A; every tap: the next
@@ -1769,7 +1778,7 @@ __global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
   // the first store (round 6: the per-element scalar adds and the serialised residual loads took
   // 35 us of the 105 us of a 64->64 ResBlock conv at 16x128x128, tools/conv3_bench.py
   // --epilogue)
-  constexpr int ITER = 128 * BN / 8 / (64 * NW);
+  constexpr int ROWS = kHoT * TH * kHoW, ITER = ROWS * BN / 8 / (64 * NW);
   const int cq = tid % (BN / 8), n = n0 + cq * 8;
   const int lim = g.N - n < 8 ? g.N - n : 8;
   float cadd[8];
@@ -1797,7 +1806,7 @@ __global__ __launch_bounds__(256, KS == 32 ? 4 : 2) void halo_conv_kernel(
 #pragma unroll
   for (int k = 0; k < ITER; ++k) {
     const int r = tid / (BN / 8) + k * (64 * NW / (BN / 8));
-    const int t = t0 + r / (kHoH * kHoW), h = h0 + (r / kHoW) % kHoH, w = w0 + r % kHoW;
+    const int t = t0 + r / (TH * kHoW), h = h0 + (r / kHoW) % TH, w = w0 + r % kHoW;
     mrow[k] = (t < g.dT && h < g.dH && lim > 0) ? (((int64_t)b * g.dT + t) * g.dH + h) * g.dW + w
                                                 : -1;
 #pragma unroll
@@ -1860,18 +1869,18 @@ int halo_ks(const GemmGeom& g, bool /*tr*/) {
   if (force == 32 || force == 64) return force;
   return (g.dW <= 32 || g.sC >= 128) ? 64 : 32;
 }
-template <bool TR, int KS>
+template <bool TR, int KS, int NW>
 void launch_halo_tile(const GemmGeom& g, const void* src, const void* wt, void* dst,
                   const float* bias, const float* ca, const void* res, hipStream_t st) {
-  const size_t lds_c = (size_t)128 * (64 + 4) * 4;
-  const size_t lds = halo_lds<3, KS>() > lds_c ? halo_lds<3, KS>() : lds_c;
-  auto kern = halo_conv_kernel<TR, KS>;
+  const size_t lds_c = (size_t)kHoT * NW * kHoW * (64 + 4) * 4;  // the epilogue's fp32 tile
+  const size_t lds = halo_lds<3, KS, NW>() > lds_c ? halo_lds<3, KS, NW>() : lds_c;
+  auto kern = halo_conv_kernel<TR, KS, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-  const int64_t tiles = (int64_t)g.B * vd_cdiv(g.dT, kHoT) * vd_cdiv(g.dH, kHoH) * (g.dW / kHoW);
+  const int64_t tiles = (int64_t)g.B * vd_cdiv(g.dT, kHoT) * vd_cdiv(g.dH, NW) * (g.dW / kHoW);
   dim3 grid((unsigned)tiles, (unsigned)vd_cdiv(g.N, 64));
-  kern<<<grid, 256, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias, ca,
-                               (const bf16_t*)res);
+  kern<<<grid, 64 * NW, lds, st>>>(g, (const bf16_t*)src, (const bf16_t*)wt, (bf16_t*)dst, bias,
+                                   ca, (const bf16_t*)res);
 }
 // (round 6, measured and removed: two taps per ring stage and barrier at three workgroups per CU
 // -- equal; a barrier-free form where each wave streams its own 16 weight rows for all 128
@@ -1880,8 +1889,13 @@ void launch_halo_tile(const GemmGeom& g, const void* src, const void* wt, void* 
 template <bool TR>
 void launch_halo(const GemmGeom& g, int ks, const void* src, const void* wt, void* dst,
                  const float* bias, const float* ca, const void* res, hipStream_t st) {
-  if (ks == 32) launch_halo_tile<TR, 32>(g, src, wt, dst, bias, ca, res, st);
-  else launch_halo_tile<TR, 64>(g, src, wt, dst, bias, ca, res, st);
+  if (conv_halo_mode() == 3) {  // A/B: 8-wave workgroups on 2 x 8 x 16 tiles
+    if (ks == 32) launch_halo_tile<TR, 32, 8>(g, src, wt, dst, bias, ca, res, st);
+    else launch_halo_tile<TR, 64, 8>(g, src, wt, dst, bias, ca, res, st);
+    return;
+  }
+  if (ks == 32) launch_halo_tile<TR, 32, 4>(g, src, wt, dst, bias, ca, res, st);
+  else launch_halo_tile<TR, 64, 4>(g, src, wt, dst, bias, ca, res, st);
 }
 
 // ----------------------------------------------------------------- 1x1 convs: streaming GEMM
@@ -2205,8 +2219,8 @@ int vd_conv_set_wgrad(int mode) {
 }
 
 int vd_conv_set_halo(int mode) {
-  if (mode < 0 || mode > 2) {
-    (void)vd::fail(VD_EINVAL, "conv halo mode %d (0, 1, 2)", mode);
+  if (mode < 0 || mode > 3) {
+    (void)vd::fail(VD_EINVAL, "conv halo mode %d (0 - 3)", mode);
     return -2;
   }
   return g_halo_mode.exchange(mode);

@@ -418,8 +418,8 @@ template <typename T, bool SILU, int U>
 __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ rstd,
-    const float* __restrict__ coef, T* __restrict__ dx, int64_t S, int C, int G, int64_t chunk_px,
-    int rows_per_iter, Drop drop_in) {
+    const float* __restrict__ coef, const T* __restrict__ dadd, T* __restrict__ dx, int64_t S,
+    int C, int G, int64_t chunk_px, int rows_per_iter, Drop drop_in) {
   const Drop drop = drop_in.resolved();
   const int nvec = C / kVec, cpg = C / G;
   const int b = blockIdx.y, tid = threadIdx.x;
@@ -450,6 +450,12 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(
         dz *= sg * (1.f + z * (1.f - sg));
       }
       v[j] = rs[j] * (ga[j] * dz - c0[j] - xh * c1[j]);
+    }
+    if (dadd) {  // the input's other gradient (a residual branch), added before the one rounding
+      float a[kVec];
+      load8(dadd + e0, a);
+#pragma unroll
+      for (int j = 0; j < kVec; ++j) v[j] += a[j];
     }
     store8(dx + e0, v);
   };
@@ -543,6 +549,15 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
                           const float* mean, const float* rstd, void* dx, float* dgamma,
                           float* dbeta, int B, int64_t S, int C, int G, int silu, float drop_p,
                           uint64_t seed, int dtype, void* workspace, void* stream) {
+  return vd_groupnorm_silu_bwd_add(x, dy, nullptr, gamma, beta, mean, rstd, dx, dgamma, dbeta, B,
+                                   S, C, G, silu, drop_p, seed, dtype, workspace, stream);
+}
+
+int vd_groupnorm_silu_bwd_add(const void* x, const void* dy, const void* dadd, const float* gamma,
+                              const float* beta, const float* mean, const float* rstd, void* dx,
+                              float* dgamma, float* dbeta, int B, int64_t S, int C, int G,
+                              int silu, float drop_p, uint64_t seed, int dtype, void* workspace,
+                              void* stream) {
   int rc = gn_check(x, B, S, C, G);
   if (rc) return rc;
   VD_REQUIRE(dy && gamma && beta && mean && rstd && dx && dgamma && dbeta && workspace,
@@ -572,12 +587,12 @@ int vd_groupnorm_silu_bwd(const void* x, const void* dy, const float* gamma, con
                                                  dbeta);                                          \
   if (silu)                                                                                      \
     gn_bwd_apply_kernel<T, true, U><<<grid, kThreads, 0, st>>>(                                  \
-        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,   \
-        p.rows_per_iter, drop);                                                                  \
+        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (const T*)dadd, (T*)dx, S, C,  \
+        G, p.chunk_px, p.rows_per_iter, drop);                                                   \
   else                                                                                           \
     gn_bwd_apply_kernel<T, false, U><<<grid, kThreads, 0, st>>>(                                 \
-        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (T*)dx, S, C, G, p.chunk_px,   \
-        p.rows_per_iter, drop)
+        (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (const T*)dadd, (T*)dx, S, C,  \
+        G, p.chunk_px, p.rows_per_iter, drop)
   return VD_DISPATCH_DTYPE(dtype, T, {
     VD_GN_BWD(1);
   });

@@ -63,6 +63,8 @@ _SIGS = {
                                    _u64, _i, _vp, _vp]),
     "vd_groupnorm_silu_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i64, _i, _i,
                                    _i, _f, _u64, _i, _vp, _vp]),
+    "vd_groupnorm_silu_bwd_add": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i64,
+                                       _i, _i, _i, _f, _u64, _i, _vp, _vp]),
     "vd_silu": (_i, [_vp, _vp, _i64, _i, _vp]),
     "vd_silu_bwd": (_i, [_vp, _vp, _vp, _i64, _i, _vp]),
     "vd_cond_concat": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),

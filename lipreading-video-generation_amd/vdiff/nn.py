@@ -259,12 +259,13 @@ class ResBlock(TimestepBlock):
     def _forward(self, x, emb):
         gn1, conv1 = self.in_layers[0], self.in_layers[2]
         gn2, drop, conv2 = self.out_layers[0], self.out_layers[2], self.out_layers[3]
-        h = ops.group_norm_silu(x, gn1.weight, gn1.bias, gn1.num_groups, gn1.eps)
+        # x also feeds the skip branch: its two gradients meet inside GN1's backward
+        h, xs = ops.group_norm_silu_pass(x, gn1.weight, gn1.bias, gn1.num_groups, gn1.eps)
         emb_out = emb[self] if isinstance(emb, EmbTable) else self.emb_layers(emb)
         h = ops.conv(h, conv1.weight, conv1.bias, conv1.stride, conv1.padding, chan_add=emb_out)
         p = drop.p if self.training else 0.0
         h = ops.group_norm_silu(h, gn2.weight, gn2.bias, gn2.num_groups, gn2.eps, dropout=p)
-        skip = self.skip_connection(x)
+        skip = self.skip_connection(xs)
         return ops.conv(h, conv2.weight, conv2.bias, conv2.stride, conv2.padding, residual=skip)
 
 
@@ -382,10 +383,11 @@ class AttentionBlock(nn.Module):
         return checkpoint(self._forward, (x, context), self.parameters(), self.use_checkpoint)
 
     def _attend(self, xf, norm, qkv_conv, proj, mode, spatial):
-        h = ops.group_norm_silu(xf, norm.weight, norm.bias, norm.num_groups, norm.eps, silu=False)
+        h, xs = ops.group_norm_silu_pass(xf, norm.weight, norm.bias, norm.num_groups, norm.eps,
+                                         silu=False)
         qkv = ops.conv(h, qkv_conv.weight, qkv_conv.bias)
         a = ops.attention(qkv, self.num_heads, mode=mode, spatial=spatial, legacy=self.legacy)
-        return ops.conv(a, proj.weight, proj.bias, residual=xf)
+        return ops.conv(a, proj.weight, proj.bias, residual=xs)
 
     def _cross(self, h, context, frames):
         """h + audio_proj_out(cross_attention(audio_q(GN(h)), audio_kv(audio tokens)))."""

@@ -192,9 +192,16 @@ def ddim_step(xt, eps, t, t_prev, acp, eta=0.0, z=None, clip=False):
 
 # --------------------------------------------------------------- GroupNorm+SiLU
 class GroupNormSiLUFn(torch.autograd.Function):
+    """y = dropout(silu(GN(x))).  With `passthrough`, forward also returns x itself (an alias)
+    for the block's residual branch: autograd then hands this backward both of x's gradients,
+    and vd_groupnorm_silu_bwd_add sums them inside the GN backward's last pass instead of the
+    separate bf16 add autograd runs where a tensor has two consumers (ResBlock: x feeds GN1 and
+    skip_connection, unet.py:264-268; AttentionBlock: x feeds norm and the residual,
+    unet.py:313-317)."""
+
     @staticmethod
     def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float,
-                seed: int):
+                seed: int, passthrough: bool = False):
         _gpu(x, gamma, beta)
         x = to_cl(x)
         B, Cc, S = x.shape[0], x.shape[1], _spatial(x)
@@ -211,23 +218,29 @@ class GroupNormSiLUFn(torch.autograd.Function):
                   _stream(x))
         ctx.save_for_backward(x, g32, b32, mean, rstd)
         ctx.cfg = (groups, silu, gamma.dtype, float(drop_p), int(seed))
+        if passthrough:
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dadd=None):
         x, g32, b32, mean, rstd = ctx.saved_tensors
         groups, silu, pdt, drop_p, seed = ctx.cfg
         dy = to_cl(dy).to(x.dtype)
+        if dadd is not None:  # x's gradient through the passthrough alias (same layout as x)
+            dadd = to_cl(dadd).to(x.dtype)
+            if dadd.stride() != x.stride():
+                dadd = torch.empty_like(x).copy_(dadd)
         B, Cc, S = x.shape[0], x.shape[1], _spatial(x)
         dx = torch.empty_like(x)
         dg = torch.empty(Cc, dtype=torch.float32, device=x.device)
         db = torch.empty_like(dg)
         ws = torch.empty(_lib.lib().vd_groupnorm_workspace_size(B, S, Cc, groups),
                          dtype=torch.uint8, device=x.device)
-        _lib.call("vd_groupnorm_silu_bwd", _p(x), _p(dy), _p(g32), _p(b32), _p(mean), _p(rstd),
-                  _p(dx), _p(dg), _p(db), B, S, Cc, groups, int(silu), drop_p, seed, _dtype(x),
-                  _p(ws), _stream(x))
-        return dx, dg.to(pdt), db.to(pdt), None, None, None, None, None
+        _lib.call("vd_groupnorm_silu_bwd_add", _p(x), _p(dy), _p(dadd), _p(g32), _p(b32),
+                  _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), B, S, Cc, groups, int(silu), drop_p,
+                  seed, _dtype(x), _p(ws), _stream(x))
+        return dx, dg.to(pdt), db.to(pdt), None, None, None, None, None, None
 
 
 def new_seed() -> int:
@@ -241,6 +254,19 @@ def group_norm_silu(x, weight, bias, groups=32, eps=1e-5, silu=True, dropout=0.0
         seed = new_seed()
     return GroupNormSiLUFn.apply(x, weight, bias, groups, eps, silu, float(dropout),
                                  int(seed or 0))
+
+
+def group_norm_silu_pass(x, weight, bias, groups=32, eps=1e-5, silu=True):
+    """(silu(GroupNorm(x)), x'): x' is x for the caller's residual branch; the gradient that
+    reaches x' is added inside the GroupNorm backward (GroupNormSiLUFn, passthrough).
+    VDIFF_GN_PASSTHROUGH=0 (read at import; A/B) returns x itself and leaves the add to
+    autograd."""
+    if not _GN_PASSTHROUGH:
+        return group_norm_silu(x, weight, bias, groups, eps, silu), x
+    return GroupNormSiLUFn.apply(x, weight, bias, groups, eps, silu, 0.0, 0, True)
+
+
+_GN_PASSTHROUGH = os.environ.get("VDIFF_GN_PASSTHROUGH", "1") != "0"
 
 
 class SiLUFn(torch.autograd.Function):
@@ -1058,11 +1084,12 @@ class attention_config:
 class conv_halo:
     """Context manager selecting which 3x3x3 stride-1 bf16 convs take the halo-tile kernel
     (vd_conv_set_halo): 0 none (the gathered-tile kernel), 1 / 2 (default) every eligible
-    shape.  Results agree up to fp32 summation order; used by tests and A/B benchmarks."""
+    shape on 4-wave 2 x 4 x 16 tiles, 3 every eligible shape on 8-wave 2 x 8 x 16 tiles.
+    Results agree up to fp32 summation order; used by tests and A/B benchmarks."""
 
     def __init__(self, mode: int):
-        if mode not in (0, 1, 2):
-            raise ValueError(f"conv halo mode {mode!r}: 0, 1 or 2")
+        if mode not in (0, 1, 2, 3):
+            raise ValueError(f"conv halo mode {mode!r}: 0, 1, 2 or 3")
         self.mode = mode
         self.prev = None
 

@@ -55,7 +55,7 @@ HALO_CASES = [i for i, c in enumerate(CASES)
               if len(c[0]) == 5 and c[2] == 3 and c[3] == 1 and c[4] == 1 and c[0][-1] % 16 == 0]
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 3])
 @pytest.mark.parametrize("case", HALO_CASES)
 def test_conv_halo_modes(case, mode):
     from vdiff import ops
@@ -65,7 +65,7 @@ def test_conv_halo_modes(case, mode):
 
 def test_conv_halo_hook_rejects_unknown():
     from vdiff import _lib, ops
-    assert _lib.lib().vd_conv_set_halo(3) == -2
+    assert _lib.lib().vd_conv_set_halo(4) == -2
     with pytest.raises(ValueError):
         ops.conv_halo(5)
 
@@ -77,8 +77,9 @@ DETERMINISM = [(64, 64, 16, 128), (192, 128, 16, 64), (256, 256, 16, 32), (200, 
                (96, 80, 5, 32)]
 
 
+@pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("shape", DETERMINISM)
-def test_halo_conv_is_deterministic(shape):
+def test_halo_conv_is_deterministic(shape, mode):
     """Bit-identical outputs over repeated launches (fwd and bwd-data) at full train-step sizes:
     every LDS read of a ring stage or halo returns before a barrier lets another wave's DMA refill
     it (vm_lgk_wait_barrier), so no launch may differ from another."""
@@ -94,17 +95,18 @@ def test_halo_conv_is_deterministic(shape):
                   ops._DT[torch.bfloat16])
     st = ops._stream(x)
     for name, src, wt, shp in (("vd_conv3d_fwd", x, wf, Co), ("vd_conv3d_bwd_data", dy, wb, Ci)):
-        outs = []
-        for _ in range(12):
-            o = torch.empty(1, T, H, H, shp, dtype=torch.bfloat16, device=dev)
-            if name == "vd_conv3d_fwd":
-                _lib.call(name, d, src.data_ptr(), wt.data_ptr(), None, None, None, o.data_ptr(), st)
-            else:
-                _lib.call(name, d, src.data_ptr(), wt.data_ptr(), o.data_ptr(), st)
-            outs.append(o)
-        torch.cuda.synchronize()
-        bad = [i for i, o in enumerate(outs) if not torch.equal(o, outs[0])]
-        assert not bad, (name, shape, bad)
+        with ops.conv_halo(mode):
+            outs = []
+            for _ in range(12):
+                o = torch.empty(1, T, H, H, shp, dtype=torch.bfloat16, device=dev)
+                if name == "vd_conv3d_fwd":
+                    _lib.call(name, d, src.data_ptr(), wt.data_ptr(), None, None, None, o.data_ptr(), st)
+                else:
+                    _lib.call(name, d, src.data_ptr(), wt.data_ptr(), o.data_ptr(), st)
+                outs.append(o)
+            torch.cuda.synchronize()
+            bad = [i for i, o in enumerate(outs) if not torch.equal(o, outs[0])]
+            assert not bad, (name, shape, bad)
 
 
 def _conv_vs_oracle(case, dtype):

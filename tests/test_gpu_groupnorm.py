@@ -80,3 +80,34 @@ def test_gn_bwd_bit_reproducible(shape):
     r2 = _run(x, w, b, True, torch.bfloat16, g)
     for a, c in zip(r1, r2):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("silu", [True, False])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(1, 64, 4, 32, 32), (2, 192, 3, 9, 11)])
+def test_gn_passthrough_adds_residual_gradient(shape, dtype, silu):
+    """Round 6: group_norm_silu_pass returns (GN(x), x'); the gradient reaching x' (a residual
+    branch) is added inside the GN backward (vd_groupnorm_silu_bwd_add) instead of by an
+    autograd add.  Against GN alone + the residual gradient added in fp32: fp32 to rounding,
+    bf16 to one rounding of the sum (the fused form rounds once, autograd's add twice)."""
+    from vdiff import ops
+    C = shape[1]
+    x = seeded(shape, 40)
+    w, b = 1 + 0.1 * seeded((C,), 41), 0.1 * seeded((C,), 42)
+    g, gr = seeded(shape, 43), seeded(shape, 44)
+    xd = ops.to_cl(x.to(dev, dtype)).requires_grad_(True)
+    wd, bd = w.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+    y, xs = ops.group_norm_silu_pass(xd, wd, bd, 32, 1e-5, silu)
+    assert xs.data_ptr() == xd.data_ptr()
+    torch.autograd.backward([y, xs], [ops.to_cl(g.to(dev, dtype)), ops.to_cl(gr.to(dev, dtype))])
+    _, dx0, dw0, db0 = _run(x, w, b, silu, torch.float32 if dtype == torch.float32 else dtype, g)
+    want = dx0 + gr.to(dtype).float()
+    tol = 1e-6 if dtype == torch.float32 else 8e-3
+    assert rel_l2(xd.grad.float().cpu(), want) < tol
+    torch.testing.assert_close(wd.grad.cpu(), dw0)
+    torch.testing.assert_close(bd.grad.cpu(), db0)
+    # no gradient through the alias: plain GN backward
+    xd2 = ops.to_cl(x.to(dev, dtype)).requires_grad_(True)
+    y2, _ = ops.group_norm_silu_pass(xd2, wd.detach(), bd.detach(), 32, 1e-5, silu)
+    y2.backward(ops.to_cl(g.to(dev, dtype)))
+    assert torch.equal(xd2.grad.float().cpu(), dx0)
