@@ -2533,15 +2533,27 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* __restri
   const int64_t row = i / ci4;  // co * taps + tap
   const int ci = (int)(i % ci4) * 4;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [&](const float4& v) {
+    a.x += v.x;
+    a.y += v.y;
+    a.z += v.z;
+    a.w += v.w;
+  };
   if (i < n4 && ci < Ci_out) {
     const float* p = part + row * Ci + ci;
-    for (int sp = grp; sp < splits; sp += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)sp * sstride);
-      a.x += v.x;
-      a.y += v.y;
-      a.z += v.z;
-      a.w += v.w;
+    // four of the group's splits in flight per iteration, added in the same ascending order
+    // (round 6: the one-load-per-iteration loop waited a full memory latency per split;
+    // bit-identical result)
+    int sp = grp;
+    for (; sp + 48 < splits; sp += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = *reinterpret_cast<const float4*>(p + (int64_t)(sp + 16 * u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u]);
     }
+    for (; sp < splits; sp += 16) add(*reinterpret_cast<const float4*>(p + (int64_t)sp * sstride));
   }
   sums[grp][oi] = a;
   __syncthreads();

@@ -277,3 +277,32 @@ def test_conv_wgrad_round4_split_rule(shape, Co, k):
     assert torch.equal(a, b)
     ref = _wgrad(ops.to_cl(x.float()), w, ops.to_cl(dy.float()), 1, pad, False)
     assert rel_l2(a, ref) < 1e-5, rel_l2(a, ref)
+
+
+@pytest.mark.parametrize("shape,Co,k", [((1, 64, 16, 128, 128), 64, 3),   # one 64-px row / step
+                                       ((1, 256, 16, 32, 32), 256, 3),    # two rows / step
+                                       ((2, 32, 4, 16, 16), 32, 3),       # four rows, two clips
+                                       ((1, 64, 3, 5, 32), 64, 3),        # H % rows != 0: round 5
+                                       ((1, 2 * 64, 4, 8, 128), 128, 3),  # two steps per row
+                                       ((1, 64, 16, 64, 64), 192, 1),     # 1x1
+                                       ((1, 96, 2, 5, 7), 48, 1)])        # 1x1, short last step
+def test_wgrad_strip_equals_round5_kernel(shape, Co, k):
+    """Round 6: the stage-unrolled weight-gradient kernel (vd_conv_set_wgrad(1), the default)
+    runs the round-5 kernel's tiles, DMA pieces and summation order, so the two are
+    bit-identical (tools/wgrad3_bench.py checks the same on every shape of the step)."""
+    from vdiff import _lib, ops
+    x = ops.to_cl(seeded(shape, 27).to(dev, torch.bfloat16))
+    w = (seeded((Co, shape[1]) + (k,) * 3, 28) / (shape[1] * k ** 3) ** 0.5).to(dev)
+    pad = k // 2
+    y = ops.conv(x, w, None, padding=pad)
+    dy = ops.to_cl(seeded(tuple(y.shape), 29).to(dev, torch.bfloat16))
+    lib = _lib.lib()
+    prev = lib.vd_conv_set_wgrad(0)
+    try:
+        a = _wgrad(x, w, dy, 1, pad, False)
+        lib.vd_conv_set_wgrad(1)
+        b = _wgrad(x, w, dy, 1, pad, False)
+    finally:
+        lib.vd_conv_set_wgrad(prev)
+    assert torch.equal(a, b)
+    assert lib.vd_conv_set_wgrad(2) == -2

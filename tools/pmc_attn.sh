@@ -13,6 +13,6 @@ G5="SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE SQ_INST_CYC
 i=0
 for G in "$G1" "$G2" "$G3" "$G4" "$G5"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $G --output-format csv -d $OUT/p$i -o pmc -- python tools/attn_bench.py 1 --calib --nocheck "$@" > $OUT/p$i.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $G --output-format csv -d $OUT/p$i -o pmc -- python tools/attn_bench.py 1 --calib --nocheck "$@" > $OUT/p$i.log 2>&1
 done
 python tools/pmc_traffic.py $OUT $OUT/pmc_traffic.json $OUT/pmc_attn.md
