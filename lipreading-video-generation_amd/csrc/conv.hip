@@ -1600,7 +1600,7 @@ __device__ __forceinline__ int h2_swz(int w) {
   else return (w >> 1) & 2;
 }
 
-template <bool TR, int KS, int NW>
+template <bool TR, int KS, int NW, bool EA = true>
 __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
     GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
     bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
@@ -1635,7 +1635,13 @@ __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
   const rsrc_t rs_a = make_rsrc(src, (uint32_t)((int64_t)g.B * g.sT * g.sH * g.sW * g.sCs * 2));
   const rsrc_t rs_b = make_rsrc(wt, (uint32_t)((int64_t)g.N * g.K * 2));
 
-  int h_off[HPW], h_c[HPW];
+  // (the chunk's channel test only matters in a ragged last channel step: recomputed there
+  // rather than held in HPW more registers through the tap loop)
+  int h_off[HPW];
+  auto h_chunk = [&](int i) {
+    const int hw = (PPP * (wave + NW * i) + lr) % kHaW;
+    return (pc ^ h2_swz<KS>(hw)) * 8;
+  };
 #pragma unroll
   for (int i = 0; i < HPW; ++i) {
     const int q = wave + NW * i, p = PPP * q + lr;
@@ -1645,13 +1651,13 @@ __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
     const bool in = q < HP && (unsigned)st < (unsigned)g.sT &&
                     (unsigned)sh < (unsigned)g.sH && (unsigned)sw < (unsigned)g.sW;
     h_off[i] = in ? (((b * g.sT + st) * g.sH + sh) * g.sW + sw) * g.sCs * 2 + c * 16 : -1;
-    h_c[i] = c * 8;
   }
   auto issue_halo = [&](int cs) {
+    const bool cfull = (cs + 1) * KS <= C;
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
       const int q = wave + NW * i;
-      const bool ok = (h_off[i] >= 0) & (cs * KS + h_c[i] < C);
+      const bool ok = (h_off[i] >= 0) & (cfull || cs * KS + h_chunk(i) < C);
       dma_lds<16>(rs_a, lds_addr(q < HP ? smem + q * 1024 : junk),
                   ok ? (uint32_t)(h_off[i] + cs * KS * 2) : 0x80000000u);
     }
@@ -1721,42 +1727,61 @@ __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
 #pragma unroll
         for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(abase[i][d][s]));
     bf16x8 af[2][NI][NS];
+    auto read_a = [&](int tp) {  // A fragments of tap tp from the halo
+      const int a = tp / 9, bb = (tp / 3) % 3, cc = tp % 3;
+      const int dt = TR ? 2 - a : a, dh = TR ? 2 - bb : bb, dw = TR ? 2 - cc : cc;
+      const int lofs = (dt * kHaH + dh) * kHaW * RB;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          af[tp & 1][i][s] = *reinterpret_cast<const bf16x8*>(smem + abase[i][dw][s] + lofs);
+    };
 #pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
       // this tap's weights (and at tap 0 the halo) landed everywhere; stage tap-1 is free
       if (wl) vm_lgk_wait_barrier<(PD - 1) * IB>();
       else vm_lgk_wait_barrier<0>();
       issue_b(cs, tap + PD);
+      const int so = (tap % NSTB) * (BN * RB);
+      if constexpr (EA) {
+        // round 6: this tap's B fragments, then the next tap's A fragments, all issued before
+        // the MFMAs (pinned by the scheduling barrier): the A reads land during this tap's
+        // MFMAs instead of being issued after their last use of the registers, where the next
+        // barrier's lgkmcnt(0) waited out their whole latency
+        if (tap == 0) read_a(0);
+        bf16x8 bfr[NS][NJ];
 #pragma unroll
-      for (int u = (tap == 0 ? 0 : 1); u < 2; ++u) {  // tap 0: its own A; every tap: the next
-        const int tp = tap + u;
-        if (tp >= TAPS) break;
-        const int a = tp / 9, bb = (tp / 3) % 3, cc = tp % 3;
-        const int dt = TR ? 2 - a : a, dh = TR ? 2 - bb : bb, dw = TR ? 2 - cc : cc;
-        const int lofs = (dt * kHaH + dh) * kHaW * RB;
-        if (u == 1 || tap == 0) {
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            bfr[s][j] = *reinterpret_cast<const bf16x8*>(smem + bbase[j][s] + so);
+        if (tap + 1 < TAPS) read_a(tap + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
 #pragma unroll
           for (int i = 0; i < NI; ++i)
 #pragma unroll
-            for (int s = 0; s < NS; ++s)
-              af[tp & 1][i][s] =
-                  *reinterpret_cast<const bf16x8*>(smem + abase[i][dw][s] + lofs);
-        }
-        if (tap == 0 && u == 0) continue;
-      }
-      const int so = (tap % NSTB) * (BN * RB);
+            for (int j = 0; j < NJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tap & 1][i][s], bfr[s][j],
+                                                                  acc[i][j], 0, 0, 0);
+      } else {  // the compiler's placement (A/B: vd_conv_set_halo(4))
+        if (tap == 0) read_a(0);
+        if (tap + 1 < TAPS) read_a(tap + 1);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        bf16x8 bfr[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(smem + bbase[j][s] + so);
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
+        for (int s = 0; s < NS; ++s) {
+          bf16x8 bfr[NJ];
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tap & 1][i][s], bfr[j],
-                                                                acc[i][j], 0, 0, 0);
+            bfr[j] = *reinterpret_cast<const bf16x8*>(smem + bbase[j][s] + so);
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tap & 1][i][s], bfr[j],
+                                                                  acc[i][j], 0, 0, 0);
+        }
       }
     }
   }
@@ -1869,12 +1894,12 @@ int halo_ks(const GemmGeom& g, bool /*tr*/) {
   if (force == 32 || force == 64) return force;
   return (g.dW <= 32 || g.sC >= 128) ? 64 : 32;
 }
-template <bool TR, int KS, int NW>
+template <bool TR, int KS, int NW, bool EA = true>
 void launch_halo_tile(const GemmGeom& g, const void* src, const void* wt, void* dst,
                   const float* bias, const float* ca, const void* res, hipStream_t st) {
   const size_t lds_c = (size_t)kHoT * NW * kHoW * (64 + 4) * 4;  // the epilogue's fp32 tile
   const size_t lds = halo_lds<3, KS, NW>() > lds_c ? halo_lds<3, KS, NW>() : lds_c;
-  auto kern = halo_conv_kernel<TR, KS, NW>;
+  auto kern = halo_conv_kernel<TR, KS, NW, EA>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int64_t tiles = (int64_t)g.B * vd_cdiv(g.dT, kHoT) * vd_cdiv(g.dH, NW) * (g.dW / kHoW);
@@ -1892,6 +1917,11 @@ void launch_halo(const GemmGeom& g, int ks, const void* src, const void* wt, voi
   if (conv_halo_mode() == 3) {  // A/B: 8-wave workgroups on 2 x 8 x 16 tiles
     if (ks == 32) launch_halo_tile<TR, 32, 8>(g, src, wt, dst, bias, ca, res, st);
     else launch_halo_tile<TR, 64, 8>(g, src, wt, dst, bias, ca, res, st);
+    return;
+  }
+  if (conv_halo_mode() == 4) {  // A/B: round-6 tap loop with the compiler's read placement
+    if (ks == 32) launch_halo_tile<TR, 32, 4, false>(g, src, wt, dst, bias, ca, res, st);
+    else launch_halo_tile<TR, 64, 4, false>(g, src, wt, dst, bias, ca, res, st);
     return;
   }
   if (ks == 32) launch_halo_tile<TR, 32, 4>(g, src, wt, dst, bias, ca, res, st);
@@ -2219,8 +2249,8 @@ int vd_conv_set_wgrad(int mode) {
 }
 
 int vd_conv_set_halo(int mode) {
-  if (mode < 0 || mode > 3) {
-    (void)vd::fail(VD_EINVAL, "conv halo mode %d (0 - 3)", mode);
+  if (mode < 0 || mode > 4) {
+    (void)vd::fail(VD_EINVAL, "conv halo mode %d (0 - 4)", mode);
     return -2;
   }
   return g_halo_mode.exchange(mode);

@@ -65,9 +65,9 @@ def test_conv_halo_modes(case, mode):
 
 def test_conv_halo_hook_rejects_unknown():
     from vdiff import _lib, ops
-    assert _lib.lib().vd_conv_set_halo(4) == -2
+    assert _lib.lib().vd_conv_set_halo(5) == -2
     with pytest.raises(ValueError):
-        ops.conv_halo(5)
+        ops.conv_halo(6)
 
 
 # (Ci, Co, T, H = W): the train step's halo shapes at both channel steps, the one that showed a
