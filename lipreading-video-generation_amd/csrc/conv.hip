@@ -1098,7 +1098,7 @@ __global__ __launch_bounds__(kThreads, PLANE ? 1 : 2) void wgrad_dma_kernel(
 // branch-free bounds test.  Same tiles, DMA pieces and summation order as wgrad_dma_kernel.
 // KIND 0: kw strip, a step is R = 64 / Wo whole image rows; 1: kw strip, a step is one 64-pixel
 // row segment (W % 64 == 0); 2: 1x1 stride-1 unpadded conv (X rows = dY rows, one tap).
-template <int RW, int COT, int NST, int KIND>
+template <int RW, int COT, int NST, int KIND, bool ER = true>
 __global__ __launch_bounds__(kThreads, 2) void wgrad_strip_kernel(WgtGeom g, int wc,
                                                                   const bf16_t* __restrict__ x,
                                                                   const bf16_t* __restrict__ dy,
@@ -1293,32 +1293,37 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_strip_kernel(WgtGeom g, int
       issue(s + NST - 1, (u + NST - 1) % NST);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[NI];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
+        bf16x8 af[NI], bfr[NT][2];
+        auto rd = [&](uint32_t a0, uint32_t a1) {
           const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(uintptr_t)(abase[ks][0][i] + u * STAGE));
+              (lds_bf16x4*)(uintptr_t)(a0 + u * STAGE));
           const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(uintptr_t)(abase[ks][1][i] + u * STAGE));
-          af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+              (lds_bf16x4*)(uintptr_t)(a1 + u * STAGE));
+          return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        };
+#pragma unroll
+        for (int i = 0; i < NI; ++i) af[i] = rd(abase[ks][0][i], abase[ks][1][i]);
+        if constexpr (ER) {
+          // round 6: every fragment of this k-half read before its first MFMA (pinned by the
+          // scheduling barrier), so one LDS latency is exposed per k-half instead of one per tap
+#pragma unroll
+          for (int tc = 0; tc < NT; ++tc)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bfr[tc][j] = rd(xbase[ks][0][tc][j], xbase[ks][1][tc][j]);
+          __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int tc = 0; tc < NT; ++tc) {
-          bf16x8 bfr[2];
+          if constexpr (!ER) {  // the compiler's placement (A/B: vd_conv_set_wgrad(2))
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_bf16x4*)(uintptr_t)(xbase[ks][0][tc][j] + u * STAGE));
-            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_bf16x4*)(uintptr_t)(xbase[ks][1][tc][j] + u * STAGE));
-            bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            for (int j = 0; j < 2; ++j) bfr[tc][j] = rd(xbase[ks][0][tc][j], xbase[ks][1][tc][j]);
           }
 #pragma unroll
           for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-              acc[tc][i][j] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[tc][i][j], 0, 0, 0);
+              acc[tc][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[tc][j],
+                                                                      acc[tc][i][j], 0, 0, 0);
         }
       }
     }
@@ -2241,8 +2246,8 @@ int vd_conv3d_fwd(const vd_conv_desc* d, const void* x, const void* w_fwd, const
 }
 
 int vd_conv_set_wgrad(int mode) {
-  if (mode < 0 || mode > 1) {
-    (void)vd::fail(VD_EINVAL, "conv wgrad mode %d (0, 1)", mode);
+  if (mode < 0 || mode > 2) {
+    (void)vd::fail(VD_EINVAL, "conv wgrad mode %d (0, 1, 2)", mode);
     return -2;
   }
   return g_wgrad_mode.exchange(mode);
@@ -2438,15 +2443,19 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     // Measured against COT = 128 and a three-stage ring: both slower (tools/conv_ab.sh).
 #define VD_WG1(COT, NST)                                                                   \
   do {                                                                                     \
-    auto kern = wgrad_strip_kernel<64, COT, NST, 2>;                                       \
+    /* 1x1: the compiler's read placement (early reads measured equal, 0.78 ms per step) */ \
+    auto kern = wgrad_strip_kernel<64, COT, NST, 2, false>;                                \
     const int lds = NST * (COT + 64) * 128;                                                \
     (void)hipFuncSetAttribute((const void*)kern,                                           \
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \
     kern<<<grid, kThreads, lds, st>>>(g, wc, (const bf16_t*)x, (const bf16_t*)dy, dw);     \
   } while (0)
     // (KIND 0 needs whole-frame steps: Ho % (64 / Wo) == 0, else the round-5 kernel)
-    const bool v2 = g_wgrad_mode.load(std::memory_order_relaxed) == 1 &&
-                    (one || wc == 64 || d->Ho % (64 / wc) == 0);
+    const int wmode = g_wgrad_mode.load(std::memory_order_relaxed);
+    const bool v2 = wmode >= 1 && (one || wc == 64 || d->Ho % (64 / wc) == 0);
+    // early fragment reads for the kw strips (round 6: 3x3x3 3.88 -> 3.70 ms per step,
+    // profiles/r06z2_wgrad3_ab_early_reads.txt); mode 2: the compiler's placement (A/B)
+    const bool wer = wmode != 2;
     if (one && v2) {  // round 6: unrolled stages (the 1x1 form of wgrad_strip_kernel)
       if (cot == 192 && w1_nst >= 4) VD_WG1(192, 4);
       else if (cot == 192) VD_WG1(192, 2);
@@ -2468,8 +2477,10 @@ static int wgrad_run(const vd_conv_desc* d, const void* x, const void* dy, float
     else if (v2) {  // round 6: unrolled stages
 #define VD_WGS(RW, COT, NST)                                                               \
   do {                                                                                     \
-    auto kern = wc == 64 ? wgrad_strip_kernel<RW, COT, NST, 1>                             \
-                         : wgrad_strip_kernel<RW, COT, NST, 0>;                            \
+    auto kern = wc == 64 ? (wer ? wgrad_strip_kernel<RW, COT, NST, 1>                      \
+                                : wgrad_strip_kernel<RW, COT, NST, 1, false>)              \
+                         : (wer ? wgrad_strip_kernel<RW, COT, NST, 0>                      \
+                                : wgrad_strip_kernel<RW, COT, NST, 0, false>);             \
     const int lds = NST * (COT + RW) * 128;                                                \
     (void)hipFuncSetAttribute((const void*)kern,                                           \
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);            \

@@ -305,4 +305,4 @@ def test_wgrad_strip_equals_round5_kernel(shape, Co, k):
     finally:
         lib.vd_conv_set_wgrad(prev)
     assert torch.equal(a, b)
-    assert lib.vd_conv_set_wgrad(2) == -2
+    assert lib.vd_conv_set_wgrad(3) == -2
