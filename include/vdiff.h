@@ -237,15 +237,16 @@ int vd_conv3d_bwd_weight_det(const vd_conv_desc* d, const void* x, const void* d
                              int Co_out, int Ci_out, void* workspace, size_t workspace_bytes,
                              void* stream);
 
-/* Which 3x3x3 stride-1 bf16 convs (fwd / bwd-data) take the halo-tile kernel: 0 none, 1 every
- * eligible shape (W % 16 == 0, pad 1), 2 (default) the shapes where it measured faster
- * (32x32 level: N <= 256; larger levels: fwd N <= 128, bwd-data with <= 64 reduction
- * channels or N <= 64).  Results are identical up to fp32 summation order.
+/* Which 3x3x3 stride-1 bf16 convs (fwd / bwd-data) take the halo-tile kernel: 0 none (the
+ * gathered tiles), 1 and 2 (default) every eligible shape (W % 16 == 0, pad 1) on 4-wave
+ * 2x4x16 tiles, 3 on 8-wave 2x8x16 tiles, 4 the 4-wave tiles with the compiler's fragment-read
+ * placement.  Modes 1-4 are bit-identical; 0 agrees up to fp32 summation order.
  * Process-wide; returns the previous mode, or -2 for an invalid one.  Initial value from env
  * VDIFF_CONV_HALO.  No reference counterpart: an A/B and test hook. */
-/* Which kernel computes the kw-strip (3x3x3 / 3x3 stride-1 bf16) weight gradients: 1 (default)
- * the round-6 kernel with the ring stages unrolled, 0 the round-5 kernel; same tiles and
- * summation order (bit-identical results).  Returns the previous mode (A/B, tests). */
+/* Which kernel computes the kw-strip (3x3x3 / 3x3 stride-1 bf16) and 1x1 weight gradients:
+ * 1 (default) the round-6 kernel with the ring stages unrolled and early fragment reads, 2 the
+ * same with the compiler's read placement, 0 the round-5 kernel; same tiles and summation
+ * order (bit-identical results).  Returns the previous mode, or -2 (A/B, tests). */
 int vd_conv_set_wgrad(int mode);
 int vd_conv_set_halo(int mode);
 
