@@ -137,6 +137,10 @@ int vd_ddim_step(const void* xt, const void* eps, const void* z, void* x_prev,
  * the counter before each replay gives every step a fresh mask, the forward
  * and backward of one step the same one.  Host-side setting; no GPU call. */
 void vd_set_dropout_counter(const uint64_t* counter);
+/* Pixel rows whose loads each GroupNorm thread keeps in flight (1 default, 2, 4); the sums are
+ * added in the same order for every value (bit-identical).  Process-wide A/B hook; returns the
+ * previous value or -2.  No reference counterpart. */
+int vd_groupnorm_set_unroll(int u);
 size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G);
 int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta,
                           void* y, float* mean, float* rstd, int B, int64_t S,

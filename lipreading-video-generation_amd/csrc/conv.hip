@@ -1605,11 +1605,10 @@ __device__ __forceinline__ int h2_swz(int w) {
   else return (w >> 1) & 2;
 }
 
-#ifndef VD_HALO_WPE32  // waves per SIMD the 32-channel-step halo kernel is compiled for (A/B)
-#define VD_HALO_WPE32 4
-#endif
+// (round 6: compiling the 32-channel-step kernel for 3 waves per SIMD instead of 4 -- no spills,
+// three workgroups per CU -- measured equal, profiles/r06z4_halo_wpe3_ab.txt)
 template <bool TR, int KS, int NW, bool EA = true>
-__global__ __launch_bounds__(64 * NW, KS == 32 ? VD_HALO_WPE32 : 2) void halo_conv_kernel(
+__global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
     GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
     bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
     const bf16_t* __restrict__ residual) {

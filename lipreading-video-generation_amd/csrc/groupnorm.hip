@@ -9,6 +9,8 @@
 // and dy + 1 write of dx.  Statistics are fp32 and combined with Chan's
 // parallel formula (per-thread shifted sums -> per-chunk -> per-sample), so
 // the variance does not cancel when |mean| >> std.
+#include <atomic>
+
 #include "vd_common.h"
 
 namespace {
@@ -28,7 +30,9 @@ static int env_int(const char* name, int dflt) {
 const int kTargetChunks = env_int("VDIFF_GN_CHUNKS", 1024);
 const int kSumPer = env_int("VDIFF_GN_SUMPER", 64);
 // The kernels take U, the pixel rows whose loads each thread keeps in flight; U = 2 / 4 measured
-// equal or slower (round 4) and only U = 1 is launched since round 5.
+// equal or slower in round 4 (DESIGN_HISTORY.md) and U = 1 is the default; round 6 re-measures
+// them per kernel through vd_groupnorm_set_unroll (A/B hook; VDIFF_GN_UNROLL at load).
+std::atomic<int> g_gn_unroll{env_int("VDIFF_GN_UNROLL", 1)};
 
 struct GNPlan {
   int rows_per_iter;  // pixel rows a WG covers per iteration
@@ -512,6 +516,14 @@ size_t vd_groupnorm_workspace_size(int B, int64_t S, int C, int G) {
 
 void vd_set_dropout_counter(const uint64_t* counter) { g_drop_ctr = counter; }
 
+int vd_groupnorm_set_unroll(int u) {
+  if (u != 1 && u != 2 && u != 4) {
+    (void)vd::fail(VD_EINVAL, "groupnorm unroll %d (1, 2, 4)", u);
+    return -2;
+  }
+  return g_gn_unroll.exchange(u);
+}
+
 int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, void* y,
                           float* mean, float* rstd, int B, int64_t S, int C, int G, float eps,
                           int silu, float drop_p, uint64_t seed, int dtype, void* workspace,
@@ -539,8 +551,15 @@ int vd_groupnorm_silu_fwd(const void* x, const float* gamma, const float* beta, 
     gn_apply_kernel<T, false, U><<<grid, kThreads, 0, st>>>((const T*)x, gamma, beta, mean,     \
                                                             rstd, (T*)y, S, C, G, p.chunk_px,   \
                                                             p.rows_per_iter, drop)
+  const int u = g_gn_unroll.load(std::memory_order_relaxed);
   return VD_DISPATCH_DTYPE(dtype, T, {
-    VD_GN_FWD(1);
+    if (u == 4) {
+      VD_GN_FWD(4);
+    } else if (u == 2) {
+      VD_GN_FWD(2);
+    } else {
+      VD_GN_FWD(1);
+    }
   });
 #undef VD_GN_FWD
 }
@@ -593,8 +612,15 @@ int vd_groupnorm_silu_bwd_add(const void* x, const void* dy, const void* dadd, c
     gn_bwd_apply_kernel<T, false, U><<<grid, kThreads, 0, st>>>(                                 \
         (const T*)x, (const T*)dy, gamma, beta, mean, rstd, coef, (const T*)dadd, (T*)dx, S, C,  \
         G, p.chunk_px, p.rows_per_iter, drop)
+  const int u = g_gn_unroll.load(std::memory_order_relaxed);
   return VD_DISPATCH_DTYPE(dtype, T, {
-    VD_GN_BWD(1);
+    if (u == 4) {
+      VD_GN_BWD(4);
+    } else if (u == 2) {
+      VD_GN_BWD(2);
+    } else {
+      VD_GN_BWD(1);
+    }
   });
 #undef VD_GN_BWD
 }

@@ -58,6 +58,7 @@ _SIGS = {
     "vd_p_sample_cosine": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i, _vp]),
     "vd_ddim_step": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _i64, _i64, _i, _vp]),
     "vd_set_dropout_counter": (None, [_vp]),
+    "vd_groupnorm_set_unroll": (_i, [_i]),
     "vd_groupnorm_workspace_size": (_sz, [_i, _i64, _i, _i]),
     "vd_groupnorm_silu_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i64, _i, _i, _f, _i, _f,
                                    _u64, _i, _vp, _vp]),

@@ -111,3 +111,27 @@ def test_gn_passthrough_adds_residual_gradient(shape, dtype, silu):
     y2, _ = ops.group_norm_silu_pass(xd2, wd.detach(), bd.detach(), 32, 1e-5, silu)
     y2.backward(ops.to_cl(g.to(dev, dtype)))
     assert torch.equal(xd2.grad.float().cpu(), dx0)
+
+
+@pytest.mark.parametrize("shape", [(1, 64, 16, 128, 128), (1, 256, 16, 32, 32), (2, 192, 3, 9, 11)])
+def test_gn_unroll_bit_identical(shape):
+    """vd_groupnorm_set_unroll (rows whose loads each thread keeps in flight) changes only the
+    load schedule: the sums are added in the same order, so y, dx, dgamma, dbeta are
+    bit-identical for U = 1, 2, 4."""
+    from vdiff import _lib
+    C = shape[1]
+    x = seeded(shape, 50)
+    w, b = 1 + 0.1 * seeded((C,), 51), 0.1 * seeded((C,), 52)
+    g = seeded(shape, 53)
+    lib = _lib.lib()
+    outs = []
+    try:
+        for u in (1, 2, 4):
+            assert lib.vd_groupnorm_set_unroll(u) in (1, 2, 4)
+            outs.append(_run(x, w, b, True, torch.bfloat16, g))
+    finally:
+        lib.vd_groupnorm_set_unroll(1)
+    assert lib.vd_groupnorm_set_unroll(3) == -2
+    for o in outs[1:]:
+        for a, c in zip(outs[0], o):
+            assert torch.equal(a, c)

@@ -59,11 +59,25 @@ def capi(C, T, H, reps=50):
 
 def main():
     if "--capi" in sys.argv:
+        # --unroll 1,4: vd_groupnorm_set_unroll values, interleaved shape by shape in this process
+        us = [1]
+        if "--unroll" in sys.argv:
+            us = [int(v) for v in sys.argv[sys.argv.index("--unroll") + 1].split(",")]
+        from vdiff import _lib
+        tot = {u: [0.0, 0.0] for u in us}
         for C, T, H in SHAPES:
-            f, b = capi(C, T, H)
             size = C * T * H * H * 2
-            print(f"GN+SiLU C-ABI C={C:4d} {T}x{H}x{H}: fwd {f:7.1f} us ({3 * size / f / 1e3:6.0f} "
-                  f"GB/s)  bwd {b:7.1f} us ({5 * size / b / 1e3:6.0f} GB/s)", flush=True)
+            for u in us:
+                _lib.lib().vd_groupnorm_set_unroll(u)
+                f, b = capi(C, T, H)
+                tot[u][0] += f
+                tot[u][1] += b
+                print(f"GN+SiLU C-ABI U={u} C={C:4d} {T}x{H}x{H}: fwd {f:7.1f} us "
+                      f"({3 * size / f / 1e3:6.0f} GB/s)  bwd {b:7.1f} us "
+                      f"({5 * size / b / 1e3:6.0f} GB/s)", flush=True)
+        _lib.lib().vd_groupnorm_set_unroll(1)
+        for u in us:
+            print(f"U={u}: fwd {tot[u][0]:.1f} us, bwd {tot[u][1]:.1f} us over the shapes")
         return
     for C, T, H in SHAPES:
         x = ops.to_cl(torch.randn(1, C, T, H, H, device="cuda").bfloat16()).requires_grad_(True)
