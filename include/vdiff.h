@@ -137,7 +137,7 @@ int vd_ddim_step(const void* xt, const void* eps, const void* z, void* x_prev,
  * the counter before each replay gives every step a fresh mask, the forward
  * and backward of one step the same one.  Host-side setting; no GPU call. */
 void vd_set_dropout_counter(const uint64_t* counter);
-/* Pixel rows whose loads each GroupNorm thread keeps in flight (1 default, 2, 4); the sums are
+/* Pixel rows whose loads each GroupNorm thread keeps in flight (1, 2 default, 4); the sums are
  * added in the same order for every value (bit-identical).  Process-wide A/B hook; returns the
  * previous value or -2.  No reference counterpart. */
 int vd_groupnorm_set_unroll(int u);

@@ -29,10 +29,12 @@ static int env_int(const char* name, int dflt) {
 }
 const int kTargetChunks = env_int("VDIFF_GN_CHUNKS", 1024);
 const int kSumPer = env_int("VDIFF_GN_SUMPER", 64);
-// The kernels take U, the pixel rows whose loads each thread keeps in flight; U = 2 / 4 measured
-// equal or slower in round 4 (DESIGN_HISTORY.md) and U = 1 is the default; round 6 re-measures
-// them per kernel through vd_groupnorm_set_unroll (A/B hook; VDIFF_GN_UNROLL at load).
-std::atomic<int> g_gn_unroll{env_int("VDIFF_GN_UNROLL", 1)};
+// The kernels take U, the pixel rows whose loads each thread keeps in flight (same summation
+// order for every U).  Round 6 re-measured them interleaved in one process (vd_groupnorm_set_unroll,
+// tools/gn_bench.py --capi --unroll, profiles/r06z5_gn_unroll.txt): over the step's 9 shapes
+// U = 2 fwd 309 / bwd 470 us, U = 1 311 / 484, U = 4 313 / 505 -- U = 2 is the default
+// (VDIFF_GN_UNROLL at load; round 4 had found U = 2 / 4 equal or slower with 2048 chunks).
+std::atomic<int> g_gn_unroll{env_int("VDIFF_GN_UNROLL", 2)};
 
 struct GNPlan {
   int rows_per_iter;  // pixel rows a WG covers per iteration

@@ -130,7 +130,7 @@ def test_gn_unroll_bit_identical(shape):
             assert lib.vd_groupnorm_set_unroll(u) in (1, 2, 4)
             outs.append(_run(x, w, b, True, torch.bfloat16, g))
     finally:
-        lib.vd_groupnorm_set_unroll(1)
+        lib.vd_groupnorm_set_unroll(2)
     assert lib.vd_groupnorm_set_unroll(3) == -2
     for o in outs[1:]:
         for a, c in zip(outs[0], o):

@@ -75,7 +75,7 @@ def main():
                 print(f"GN+SiLU C-ABI U={u} C={C:4d} {T}x{H}x{H}: fwd {f:7.1f} us "
                       f"({3 * size / f / 1e3:6.0f} GB/s)  bwd {b:7.1f} us "
                       f"({5 * size / b / 1e3:6.0f} GB/s)", flush=True)
-        _lib.lib().vd_groupnorm_set_unroll(1)
+        _lib.lib().vd_groupnorm_set_unroll(2)
         for u in us:
             print(f"U={u}: fwd {tot[u][0]:.1f} us, bwd {tot[u][1]:.1f} us over the shapes")
         return
