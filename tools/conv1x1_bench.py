@@ -27,7 +27,7 @@ def timeit(fn, reps=20):
 
 tag = "pw" if os.environ.get("VDIFF_CONV_PW", "1") != "0" else "igemm"
 for Ci, Co, P in ((64, 192, 262144), (64, 64, 262144), (128, 64, 262144), (128, 384, 65536),
-                  (128, 128, 65536)):
+                  (128, 128, 65536), (256, 768, 16384), (256, 256, 16384)):
     x = ops.to_cl(torch.randn(1, Ci, P, device="cuda", dtype=torch.bfloat16))
     w = torch.nn.Parameter(torch.randn(Co, Ci, 1, device="cuda") / Ci ** 0.5, requires_grad=False)
     b = torch.randn(Co, device="cuda")
@@ -44,3 +44,20 @@ for Ci, Co, P in ((64, 192, 262144), (64, 64, 262144), (128, 64, 262144), (128, 
     print(f"{tag:6s} {Ci:4d}->{Co:4d} x {P}: fwd {ms_f * 1e3:7.1f} us {gb / ms_f * 1e3:6.0f} GB/s"
           f"  bwd-data {ms_b * 1e3:7.1f} us {gb / ms_b * 1e3:6.0f} GB/s  rel-L2 {err:.1e}",
           flush=True)
+
+# proj_out with the block's residual fused into the store (AttentionBlock, unet.py:317):
+# GB/s counts X + residual in + Y out
+tag_r = tag
+for C, P in ((64, 262144), (128, 65536), (256, 16384)):
+    x = ops.to_cl(torch.randn(1, C, P, device="cuda", dtype=torch.bfloat16))
+    r = ops.to_cl(torch.randn(1, C, P, device="cuda", dtype=torch.bfloat16))
+    w = torch.nn.Parameter(torch.randn(C, C, 1, device="cuda") / C ** 0.5, requires_grad=False)
+    b = torch.randn(C, device="cuda")
+    with ops.frozen_weights():
+        y = ops.conv(x, w, b, residual=r)
+        ref = (torch.einsum("oc,cp->op", w[:, :, 0], x[0].float()) + b[:, None] + r[0].float())
+        err = float((y[0].float() - ref).norm() / ref.norm())
+        ms_f = timeit(lambda: ops.conv(x, w, b, residual=r))
+    gb = 3 * P * C * 2 / 1e9
+    print(f"{tag_r:6s} proj {C:4d}->{C:4d} x {P} + residual: fwd {ms_f * 1e3:7.1f} us "
+          f"{gb / ms_f * 1e3:6.0f} GB/s  rel-L2 {err:.1e}", flush=True)
