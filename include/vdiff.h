@@ -244,7 +244,8 @@ int vd_conv3d_bwd_weight_det(const vd_conv_desc* d, const void* x, const void* d
 /* Which 3x3x3 stride-1 bf16 convs (fwd / bwd-data) take the halo-tile kernel: 0 none (the
  * gathered tiles), 1 and 2 (default) every eligible shape (W % 16 == 0, pad 1) on 4-wave
  * 2x4x16 tiles, 3 on 8-wave 2x8x16 tiles, 4 the 4-wave tiles with the compiler's fragment-read
- * placement.  Modes 1-4 are bit-identical; 0 agrees up to fp32 summation order.
+ * placement, 5 the forward without early next-step halo pieces.  Modes 1-5 are bit-identical;
+ * 0 agrees up to fp32 summation order.
  * Process-wide; returns the previous mode, or -2 for an invalid one.  Initial value from env
  * VDIFF_CONV_HALO.  No reference counterpart: an A/B and test hook. */
 /* Which kernel computes the kw-strip (3x3x3 / 3x3 stride-1 bf16) and 1x1 weight gradients:

@@ -1607,7 +1607,7 @@ __device__ __forceinline__ int h2_swz(int w) {
 
 // (round 6: compiling the 32-channel-step kernel for 3 waves per SIMD instead of 4 -- no spills,
 // three workgroups per CU -- measured equal, profiles/r06z4_halo_wpe3_ab.txt)
-template <bool TR, int KS, int NW, bool EA = true>
+template <bool TR, int KS, int NW, bool EA = true, bool EH = false>
 __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
     GemmGeom g, const bf16_t* __restrict__ src, const bf16_t* __restrict__ wt,
     bf16_t* __restrict__ dst, const float* __restrict__ bias, const float* __restrict__ chan_add,
@@ -1659,10 +1659,21 @@ __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
                     (unsigned)sh < (unsigned)g.sH && (unsigned)sw < (unsigned)g.sW;
     h_off[i] = in ? (((b * g.sT + st) * g.sH + sh) * g.sW + sw) * g.sCs * 2 + c * 16 : -1;
   }
-  auto issue_halo = [&](int cs) {
+  // EH (round 6, forward only): the next channel step's first halo pieces -- wholly inside halo
+  // frames 0-1, which the forward's taps 0-8 read first and no tap from 18 on reads -- are
+  // issued at tap 18 of the current step, so a step boundary waits only for the rest.  The
+  // split is by piece index i (the same on every wave, so the vmcnt counts are uniform): pieces
+  // i < IE hold px < 16 IE NW - 1, inside frames 0-1 for every wave and covering the rows the
+  // first three taps (dh = 0) read.
+  constexpr int IE = ((2 * kHaH * kHaW) / PPP - NW) / NW + 1, NL = HPW - IE;
+  static_assert(!EH || (!TR && EA && NW == 4 && (IE - 1) * NW + NW - 1 < (2 * kHaH * kHaW) / PPP &&
+                        IE * NW * PPP >= kHaW * (kHaH + 3 + 1)),
+                "early halo pieces: frames 0-1 only, covering the dh = 0 taps");
+  auto issue_halo = [&](int cs, int i0, int i1) {
     const bool cfull = (cs + 1) * KS <= C;
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
+      if (i < i0 || i >= i1) continue;
       const int q = wave + NW * i;
       const bool ok = (h_off[i] >= 0) & (cfull || cs * KS + h_chunk(i) < C);
       dma_lds<16>(rs_a, lds_addr(q < HP ? smem + q * 1024 : junk),
@@ -1722,9 +1733,12 @@ __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
   vm_drain();
   for (int cs = 0; cs < csteps; ++cs) {
     lgk_wait_barrier();  // every wave's reads of the previous step's halo and ring returned
-    issue_halo(cs);
+    // pre: this step's early pieces were issued at the previous step's tap 18
+    const bool pre = EH && cs > 0, nxt = EH && cs + 1 < csteps;
+    if (!pre) issue_halo(cs, 0, HPW);
 #pragma unroll
     for (int i = 0; i < PD; ++i) issue_b(cs, i);
+    if (pre) issue_halo(cs, IE, HPW);  // after B0 / B1: tap 0 waits for B0 only
     // opaque per channel step: the compiler would otherwise hoist all 27 x NI per-tap fragment
     // addresses out of the loop into VGPRs instead of folding the tap offsets into ds_read
 #pragma unroll
@@ -1747,9 +1761,21 @@ __global__ __launch_bounds__(64 * NW, KS == 32 ? 4 : 2) void halo_conv_kernel(
 #pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
       // this tap's weights (and at tap 0 the halo) landed everywhere; stage tap-1 is free
-      if (wl) vm_lgk_wait_barrier<(PD - 1) * IB>();
-      else vm_lgk_wait_barrier<0>();
+      if constexpr (EH) {
+        // newer than this tap's weight pieces: the late halo pieces (taps 0, 1 of a step whose
+        // early pieces came before) or the next step's early pieces (taps 19, 20)
+        if ((tap == 0 || tap == 1) && pre) vm_lgk_wait_barrier<(PD - 1) * IB + NL>();
+        else if ((tap == 19 || tap == 20) && nxt) vm_lgk_wait_barrier<(PD - 1) * IB + IE>();
+        else vm_lgk_wait_barrier<(PD - 1) * IB>();
+      } else if (wl) {
+        vm_lgk_wait_barrier<(PD - 1) * IB>();
+      } else {
+        vm_lgk_wait_barrier<0>();
+      }
       issue_b(cs, tap + PD);
+      if constexpr (EH) {
+        if (tap == 18 && nxt) issue_halo(cs + 1, 0, IE);  // frames 0-1 are free from tap 18 on
+      }
       const int so = (tap % NSTB) * (BN * RB);
       if constexpr (EA) {
         // round 6: this tap's B fragments, then the next tap's A fragments, all issued before
@@ -1901,12 +1927,12 @@ int halo_ks(const GemmGeom& g, bool /*tr*/) {
   if (force == 32 || force == 64) return force;
   return (g.dW <= 32 || g.sC >= 128) ? 64 : 32;
 }
-template <bool TR, int KS, int NW, bool EA = true>
+template <bool TR, int KS, int NW, bool EA = true, bool EH = false>
 void launch_halo_tile(const GemmGeom& g, const void* src, const void* wt, void* dst,
                   const float* bias, const float* ca, const void* res, hipStream_t st) {
   const size_t lds_c = (size_t)kHoT * NW * kHoW * (64 + 4) * 4;  // the epilogue's fp32 tile
   const size_t lds = halo_lds<3, KS, NW>() > lds_c ? halo_lds<3, KS, NW>() : lds_c;
-  auto kern = halo_conv_kernel<TR, KS, NW, EA>;
+  auto kern = halo_conv_kernel<TR, KS, NW, EA, EH>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int64_t tiles = (int64_t)g.B * vd_cdiv(g.dT, kHoT) * vd_cdiv(g.dH, NW) * (g.dW / kHoW);
@@ -1930,6 +1956,13 @@ void launch_halo(const GemmGeom& g, int ks, const void* src, const void* wt, voi
     if (ks == 32) launch_halo_tile<TR, 32, 4, false>(g, src, wt, dst, bias, ca, res, st);
     else launch_halo_tile<TR, 64, 4, false>(g, src, wt, dst, bias, ca, res, st);
     return;
+  }
+  if constexpr (!TR) {
+    if (conv_halo_mode() != 5) {  // forward: early halo pieces (mode 5: without, A/B)
+      if (ks == 32) launch_halo_tile<TR, 32, 4, true, true>(g, src, wt, dst, bias, ca, res, st);
+      else launch_halo_tile<TR, 64, 4, true, true>(g, src, wt, dst, bias, ca, res, st);
+      return;
+    }
   }
   if (ks == 32) launch_halo_tile<TR, 32, 4>(g, src, wt, dst, bias, ca, res, st);
   else launch_halo_tile<TR, 64, 4>(g, src, wt, dst, bias, ca, res, st);
@@ -2256,8 +2289,8 @@ int vd_conv_set_wgrad(int mode) {
 }
 
 int vd_conv_set_halo(int mode) {
-  if (mode < 0 || mode > 4) {
-    (void)vd::fail(VD_EINVAL, "conv halo mode %d (0 - 4)", mode);
+  if (mode < 0 || mode > 5) {
+    (void)vd::fail(VD_EINVAL, "conv halo mode %d (0 - 5)", mode);
     return -2;
   }
   return g_halo_mode.exchange(mode);

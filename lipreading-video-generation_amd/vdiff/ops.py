@@ -1085,12 +1085,13 @@ class conv_halo:
     """Context manager selecting which 3x3x3 stride-1 bf16 convs take the halo-tile kernel
     (vd_conv_set_halo): 0 none (the gathered-tile kernel), 1 / 2 (default) every eligible
     shape on 4-wave 2 x 4 x 16 tiles, 3 every eligible shape on 8-wave 2 x 8 x 16 tiles, 4 the
-    4-wave tiles with the compiler's fragment-read placement (A/B).
+    4-wave tiles with the compiler's fragment-read placement, 5 the forward without the early
+    next-step halo pieces (A/B).
     Results agree up to fp32 summation order; used by tests and A/B benchmarks."""
 
     def __init__(self, mode: int):
-        if mode not in (0, 1, 2, 3, 4):
-            raise ValueError(f"conv halo mode {mode!r}: 0 - 4")
+        if mode not in (0, 1, 2, 3, 4, 5):
+            raise ValueError(f"conv halo mode {mode!r}: 0 - 5")
         self.mode = mode
         self.prev = None
 

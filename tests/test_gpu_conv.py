@@ -55,7 +55,7 @@ HALO_CASES = [i for i, c in enumerate(CASES)
               if len(c[0]) == 5 and c[2] == 3 and c[3] == 1 and c[4] == 1 and c[0][-1] % 16 == 0]
 
 
-@pytest.mark.parametrize("mode", [0, 1, 3])
+@pytest.mark.parametrize("mode", [0, 1, 3, 5])
 @pytest.mark.parametrize("case", HALO_CASES)
 def test_conv_halo_modes(case, mode):
     from vdiff import ops
@@ -65,9 +65,9 @@ def test_conv_halo_modes(case, mode):
 
 def test_conv_halo_hook_rejects_unknown():
     from vdiff import _lib, ops
-    assert _lib.lib().vd_conv_set_halo(5) == -2
+    assert _lib.lib().vd_conv_set_halo(6) == -2
     with pytest.raises(ValueError):
-        ops.conv_halo(6)
+        ops.conv_halo(7)
 
 
 # (Ci, Co, T, H = W): the train step's halo shapes at both channel steps, the one that showed a
@@ -77,7 +77,7 @@ DETERMINISM = [(64, 64, 16, 128), (192, 128, 16, 64), (256, 256, 16, 32), (200, 
                (96, 80, 5, 32)]
 
 
-@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("mode", [2, 3, 5])
 @pytest.mark.parametrize("shape", DETERMINISM)
 def test_halo_conv_is_deterministic(shape, mode):
     """Bit-identical outputs over repeated launches (fwd and bwd-data) at full train-step sizes:
