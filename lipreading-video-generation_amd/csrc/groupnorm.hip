@@ -185,7 +185,23 @@ __global__ __launch_bounds__(kThreads) void gn_finalize_kernel(const float* __re
   __shared__ Stat sh[kThreads / 64];
   const int g = blockIdx.x, b = blockIdx.y;
   Stat a{0.f, 0.f, 0.f};
-  for (int k = threadIdx.x; k < nchunk; k += kThreads) {
+  // the first four strided partials' loads all in flight before the (same-order) combines
+  // (round 6: the loop waited a memory latency per partial; nchunk <= 1024 = 4 x 256)
+  constexpr int PRE = 4;
+  Stat v[PRE];
+#pragma unroll
+  for (int u = 0; u < PRE; ++u) {
+    const int k = threadIdx.x + u * kThreads;
+    v[u] = Stat{0.f, 0.f, 0.f};
+    if (k < nchunk) {
+      const float* p = part + (((int64_t)b * nchunk + k) * G + g) * 3;
+      v[u] = Stat{p[0], p[1], p[2]};
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PRE; ++u)
+    if (threadIdx.x + u * kThreads < nchunk) a = chan(a, v[u]);
+  for (int k = threadIdx.x + PRE * kThreads; k < nchunk; k += kThreads) {
     const float* p = part + (((int64_t)b * nchunk + k) * G + g) * 3;
     a = chan(a, Stat{p[0], p[1], p[2]});
   }
@@ -358,7 +374,21 @@ __global__ __launch_bounds__(1024) void gn_bwd_sum_kernel(const float* __restric
   if (k1 > nchunk) k1 = nchunk;
   float2 a = make_float2(0.f, 0.f);
   if (c < C) {
-    for (int k = k0 + kl; k < k1; k += 16) {
+    int k = k0 + kl;
+    // four chunk rows' loads in flight per iteration, added in the same order (round 6)
+    for (; k + 48 < k1; k += 64) {
+      float2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = *reinterpret_cast<const float2*>(
+            part + (((int64_t)b * nchunk + k + 16 * u) * C + c) * 2);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a.x += v[u].x;
+        a.y += v[u].y;
+      }
+    }
+    for (; k < k1; k += 16) {
       const float2 v = *reinterpret_cast<const float2*>(part + (((int64_t)b * nchunk + k) * C + c) * 2);
       a.x += v.x;
       a.y += v.y;
